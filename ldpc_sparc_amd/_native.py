@@ -1,0 +1,176 @@
+"""ctypes binding of libldpc_sparc_amd.so (the C ABI in include/ldpc_sparc_amd.h).
+
+This is the only way the Python host layer reaches the GPU.  There is no CPU
+fallback: if the library is missing or no GPU is visible, every decode raises.
+"""
+import ctypes as ct
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("LDPC_SPARC_AMD_LIB", os.path.join(_HERE, "_lib", "libldpc_sparc_amd.so"))
+
+SG_SUMPROD, SG_SUMPROD2, SG_MINSUM = 0, 1, 2
+SG_F64, SG_F32 = 0, 1
+DECTYPES = {"sumprod": SG_SUMPROD, "sumprod2": SG_SUMPROD2, "minsum": SG_MINSUM}
+
+_lib = None
+
+dp = ct.POINTER(ct.c_double)
+lp = ct.POINTER(ct.c_long)
+vp = ct.c_void_p
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def _sig(lib, name, restype, argtypes):
+    f = getattr(lib, name)
+    f.restype = restype
+    f.argtypes = argtypes
+    return f
+
+
+# (name, restype, argtypes) of every symbol include/ldpc_sparc_amd.h declares.
+SIGNATURES = [
+    ("sg_last_error", ct.c_char_p, []),
+    ("sg_version", ct.c_char_p, []),
+    ("sg_device_count", ct.c_int, [ct.POINTER(ct.c_int)]),
+    ("sg_set_device", ct.c_int, [ct.c_int]),
+    ("sg_get_stream", ct.c_int, [ct.POINTER(vp)]),
+    ("sg_malloc", ct.c_int, [ct.POINTER(vp), ct.c_size_t]),
+    ("sg_free", ct.c_int, [vp]),
+    ("sg_memcpy_h2d", ct.c_int, [vp, vp, ct.c_size_t, vp]),
+    ("sg_memcpy_d2h", ct.c_int, [vp, vp, ct.c_size_t, vp]),
+    ("sg_memset", ct.c_int, [vp, ct.c_int, ct.c_size_t, vp]),
+    ("sg_stream_synchronize", ct.c_int, [vp]),
+    ("sg_event_create", ct.c_int, [ct.POINTER(vp)]),
+    ("sg_event_destroy", ct.c_int, [vp]),
+    ("sg_event_record", ct.c_int, [vp, vp]),
+    ("sg_event_elapsed_ms", ct.c_int, [vp, vp, ct.POINTER(ct.c_float)]),
+    ("sg_ldpc_graph_create", ct.c_int, [vp, vp, vp, ct.c_int, ct.c_int, ct.c_int, ct.POINTER(vp)]),
+    ("sg_ldpc_graph_destroy", ct.c_int, [vp]),
+    ("sg_ldpc_graph_info", ct.c_int, [vp] + [ct.POINTER(ct.c_int)] * 5),
+    ("sg_ldpc_decode", ct.c_int, [vp, ct.c_int, ct.c_int, vp, ct.c_int, ct.c_int, ct.c_double, vp, vp]),
+    ("sg_ldpc_decode_device", ct.c_int,
+     [vp, ct.c_int, ct.c_int, vp, ct.c_int, ct.c_int, ct.c_double, vp, vp, vp]),
+    ("sg_ldpc_count_errors_device", ct.c_int,
+     [vp, ct.c_int, vp, vp, vp, ct.c_int, ct.c_int, vp, vp]),
+    ("sumprod", ct.c_int, [dp, lp, lp, lp, ct.c_int, ct.c_int, ct.c_int, dp, ct.c_int]),
+    ("sumprod2", ct.c_int, [dp, lp, lp, lp, ct.c_int, ct.c_int, ct.c_int, dp, ct.c_int]),
+    ("minsum", ct.c_int, [dp, lp, lp, lp, ct.c_int, ct.c_int, ct.c_int, dp, ct.c_double, ct.c_int]),
+    ("Lxor", ct.c_double, [ct.c_double, ct.c_double, ct.c_int]),
+    ("Lxfb", ct.c_double, [dp, ct.c_long, ct.c_int]),
+]
+
+
+def lib():
+    """Load the shared library (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeError(
+                f"{LIB_PATH} not found: build it with `make -C ldpc_sparc_amd/csrc` "
+                "(or __graft_entry__.build()); there is no CPU fallback")
+        L = ct.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            _sig(L, name, res, args)
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().sg_last_error().decode(errors="replace")
+        raise NativeError(f"libldpc_sparc_amd error {rc}: {msg}")
+    return rc
+
+
+def device_count():
+    n = ct.c_int(0)
+    check(lib().sg_device_count(ct.byref(n)))
+    return n.value
+
+
+def require_gpu():
+    if device_count() <= 0:
+        raise NativeError("no GPU visible: ldpc_sparc_amd decodes only on MI355X (gfx950); "
+                          "there is no CPU fallback")
+
+
+def ptr(a):
+    return ct.c_void_p(a.ctypes.data) if a is not None else ct.c_void_p(0)
+
+
+class DeviceBuffer:
+    """A device allocation owned by Python (freed on GC)."""
+
+    def __init__(self, nbytes):
+        self.nbytes = int(nbytes)
+        p = ct.c_void_p()
+        check(lib().sg_malloc(ct.byref(p), self.nbytes))
+        self.ptr = p
+
+    @classmethod
+    def from_array(cls, arr, stream=None):
+        arr = np.ascontiguousarray(arr)
+        buf = cls(arr.nbytes)
+        buf.upload(arr, stream)
+        return buf
+
+    def upload(self, arr, stream=None):
+        arr = np.ascontiguousarray(arr)
+        assert arr.nbytes <= self.nbytes
+        check(lib().sg_memcpy_h2d(self.ptr, ptr(arr), arr.nbytes, stream))
+
+    def download(self, out, stream=None):
+        assert out.flags.c_contiguous and out.nbytes <= self.nbytes
+        check(lib().sg_memcpy_d2h(ptr(out), self.ptr, out.nbytes, stream))
+        return out
+
+    def zero(self, stream=None):
+        check(lib().sg_memset(self.ptr, 0, self.nbytes, stream))
+
+    def free(self):
+        if self.ptr is not None and self.ptr.value:
+            try:
+                lib().sg_free(self.ptr)
+            except Exception:
+                pass
+        self.ptr = None
+
+    def __del__(self):
+        self.free()
+
+
+def synchronize(stream=None):
+    check(lib().sg_stream_synchronize(stream))
+
+
+def library_stream():
+    s = ct.c_void_p()
+    check(lib().sg_get_stream(ct.byref(s)))
+    return s
+
+
+class Event:
+    def __init__(self):
+        e = ct.c_void_p()
+        check(lib().sg_event_create(ct.byref(e)))
+        self.ev = e
+
+    def record(self, stream=None):
+        check(lib().sg_event_record(self.ev, stream))
+
+    def elapsed_ms(self, later):
+        ms = ct.c_float()
+        check(lib().sg_event_elapsed_ms(self.ev, later.ev, ct.byref(ms)))
+        return ms.value
+
+    def __del__(self):
+        try:
+            lib().sg_event_destroy(self.ev)
+        except Exception:
+            pass

@@ -1,0 +1,182 @@
+// Runtime entry points of the C ABI: errors, devices, streams, memory, events.
+#include <mutex>
+#include <vector>
+
+#include "common.hpp"
+
+namespace sg {
+
+static thread_local std::string g_err;
+
+void set_error(const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+
+int fail(int code, const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+static std::mutex g_mu;
+static std::vector<hipStream_t> g_streams;
+static std::vector<int> g_cus;
+
+int ensure_device() {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0)
+        return fail(SG_ERR_NO_DEVICE,
+                    "no GPU visible to the HIP runtime (%s); libldpc_sparc_amd has no CPU path",
+                    e == hipSuccess ? "0 devices" : hipGetErrorString(e));
+    return SG_OK;
+}
+
+static int current_device() {
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess)
+        return -1;
+    return d;
+}
+
+hipStream_t lib_stream() {
+    int d = current_device();
+    if (d < 0)
+        return nullptr;
+    std::lock_guard<std::mutex> lk(g_mu);
+    if ((int)g_streams.size() <= d)
+        g_streams.resize(d + 1, nullptr);
+    if (!g_streams[d]) {
+        hipStream_t s;
+        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
+            return nullptr;
+        g_streams[d] = s;
+    }
+    return g_streams[d];
+}
+
+int device_cu_count() {
+    int d = current_device();
+    if (d < 0)
+        return 256;
+    std::lock_guard<std::mutex> lk(g_mu);
+    if ((int)g_cus.size() <= d)
+        g_cus.resize(d + 1, 0);
+    if (!g_cus[d]) {
+        int cu = 0;
+        if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || cu <= 0)
+            cu = 256;
+        g_cus[d] = cu;
+    }
+    return g_cus[d];
+}
+
+}  // namespace sg
+
+using namespace sg;
+
+extern "C" {
+
+const char *sg_last_error(void) { return g_err.c_str(); }
+const char *sg_version(void) { return "ldpc_sparc_amd 0.1 (gfx950)"; }
+
+int sg_device_count(int *count) {
+    SG_CHECK_ARG(count, "count is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    *count = (e == hipSuccess) ? n : 0;
+    return SG_OK;
+}
+
+int sg_set_device(int device) {
+    SG_TRY(ensure_device());
+    SG_HIP(hipSetDevice(device));
+    return SG_OK;
+}
+
+int sg_get_stream(void **stream) {
+    SG_CHECK_ARG(stream, "stream is NULL");
+    SG_TRY(ensure_device());
+    *stream = (void *)lib_stream();
+    return *stream ? SG_OK : fail(SG_ERR_HIP, "could not create the library stream");
+}
+
+int sg_malloc(void **dptr, size_t bytes) {
+    SG_CHECK_ARG(dptr, "dptr is NULL");
+    SG_TRY(ensure_device());
+    *dptr = nullptr;
+    SG_HIP(hipMalloc(dptr, bytes ? bytes : 1));
+    return SG_OK;
+}
+
+int sg_free(void *dptr) {
+    if (!dptr)
+        return SG_OK;
+    SG_HIP(hipFree(dptr));
+    return SG_OK;
+}
+
+int sg_memcpy_h2d(void *dst, const void *src, size_t bytes, void *stream) {
+    SG_TRY(ensure_device());
+    hipStream_t s = pick_stream(stream);
+    SG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+    SG_HIP(hipStreamSynchronize(s));
+    return SG_OK;
+}
+
+int sg_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream) {
+    SG_TRY(ensure_device());
+    hipStream_t s = pick_stream(stream);
+    SG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    return SG_OK;
+}
+
+int sg_memset(void *dptr, int value, size_t bytes, void *stream) {
+    SG_TRY(ensure_device());
+    SG_HIP(hipMemsetAsync(dptr, value, bytes, pick_stream(stream)));
+    return SG_OK;
+}
+
+int sg_stream_synchronize(void *stream) {
+    SG_TRY(ensure_device());
+    SG_HIP(hipStreamSynchronize(pick_stream(stream)));
+    return SG_OK;
+}
+
+int sg_event_create(void **ev) {
+    SG_CHECK_ARG(ev, "ev is NULL");
+    SG_TRY(ensure_device());
+    hipEvent_t e;
+    SG_HIP(hipEventCreate(&e));
+    *ev = (void *)e;
+    return SG_OK;
+}
+
+int sg_event_destroy(void *ev) {
+    if (ev)
+        SG_HIP(hipEventDestroy((hipEvent_t)ev));
+    return SG_OK;
+}
+
+int sg_event_record(void *ev, void *stream) {
+    SG_HIP(hipEventRecord((hipEvent_t)ev, pick_stream(stream)));
+    return SG_OK;
+}
+
+int sg_event_elapsed_ms(void *start, void *stop, float *ms) {
+    SG_HIP(hipEventSynchronize((hipEvent_t)stop));
+    SG_HIP(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));
+    return SG_OK;
+}
+
+}  // extern "C"
