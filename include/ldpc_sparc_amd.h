@@ -106,6 +106,55 @@ int minsum(double *ch, long *vdeg, long *cdeg, long *intrlv, int Nv, int Nc, int
 double Lxor(double L1, double L2, int corr_flag);
 double Lxfb(double *L, long dc, int corr_flag);
 
+
+/* -------------------------------------------------------------------- AMP */
+typedef struct sg_amp_plan sg_amp_plan;
+
+/* Design of a real SPARC with sub-sampled DCT operator (sparc.py:703-880):
+ * base matrix W (ndim 0: scalar P; 1: power allocation vector of Lc blocks;
+ * 2: spatially coupled Lr x Lc matrix), one transform per nonzero entry of W
+ * in row-major order, whose row/column orders are order0[t][Mr] and
+ * order1[t][Mc] exactly as generate_ordering (sparc.py:735-775) draws them
+ * (Mr = n or n/Lr, Mc = L*M/Lc).  precision SG_F64 follows the reference's
+ * double arithmetic; SG_F32 is the throughput path. */
+int sg_amp_plan_create(int ndim, const double *W, int Lr, int Lc, int L, int M, int n,
+                       const uint32_t *order0, const uint32_t *order1, int precision,
+                       sg_amp_plan **out);
+int sg_amp_plan_destroy(sg_amp_plan *p);
+int sg_amp_plan_info(const sg_amp_plan *p, int *w, int *nT, int *Mr, int *Mc, int *P, int *Q);
+
+/* Batched AMP decode (sparc.py:883-999, one call per codeword in the
+ * reference): y[B][n] received words sharing the plan's design; true_idx
+ * [B][L] (optional) the transmitted section indices, used for NMSE.
+ * Outputs: map_idx[B][L] final MAP section indices (argmax of s, sparc.py:997),
+ * t_final[B], nmse[B][t_max][Lc], psi[B][Lc] (sparc.py:999 return values). */
+int sg_amp_decode(sg_amp_plan *p, const double *y, int B, const int32_t *true_idx, double awgn_var,
+                  int t_max, double rtol, int phi_method, int32_t *map_idx, int32_t *t_final,
+                  double *nmse, double *psi);
+/* Device variant: d_y in the plan precision (float or double), all outputs
+ * device-resident (any output may be NULL). */
+int sg_amp_decode_device(sg_amp_plan *p, const void *d_y, int B, const int32_t *d_true_idx,
+                         double awgn_var, int t_max, double rtol, int phi_method,
+                         int32_t *d_map_idx, int32_t *d_t_final, double *d_nmse, double *d_psi,
+                         void *stream);
+/* Design operators (the Ab / Az closures of sparc_transforms, sparc.py:786-875):
+ * transpose 0: in[B][L*M] -> out[B][n];  transpose 1: in[B][n] -> out[B][L*M]. */
+int sg_amp_apply(sg_amp_plan *p, int transpose, const double *in, int B, double *out);
+int sg_amp_apply_device(sg_amp_plan *p, int transpose, const void *d_in, int B, void *d_out,
+                        void *stream);
+/* Adds {section errors, bit errors (popcount of index XOR, MSB-first bits as
+ * sparc.py:182-197), codeword errors, sum of t_final} into d_counts[4]. */
+int sg_amp_count_errors_device(const int32_t *d_map_idx, const int32_t *d_true_idx,
+                               const int32_t *d_t_final, int B, int L, int logM, int64_t *d_counts,
+                               void *stream);
+
+/* Stand-alone section estimators, double precision on the GPU:
+ * out[l*M+j] = scale * softmax_j(x[l*M : (l+1)*M])  (msg_vector_mmse_estimator,
+ * sparc.py:429-432 / sparc_new.py:1058-1066 with x = s/tau);
+ * idx[l] = argmax_j s[l*M+j], first maximum (msg_vector_map_estimator, sparc.py:485-487). */
+int sg_section_softmax(const double *x, int L, int M, double scale, double *out);
+int sg_section_argmax(const double *x, int L, int M, int32_t *idx);
+
 #ifdef __cplusplus
 }
 #endif

@@ -62,6 +62,19 @@ SIGNATURES = [
     ("sumprod2", ct.c_int, [dp, lp, lp, lp, ct.c_int, ct.c_int, ct.c_int, dp, ct.c_int]),
     ("minsum", ct.c_int, [dp, lp, lp, lp, ct.c_int, ct.c_int, ct.c_int, dp, ct.c_double, ct.c_int]),
     ("Lxor", ct.c_double, [ct.c_double, ct.c_double, ct.c_int]),
+    ("sg_amp_plan_create", ct.c_int, [ct.c_int, vp, ct.c_int, ct.c_int, ct.c_int, ct.c_int, ct.c_int,
+                                      vp, vp, ct.c_int, ct.POINTER(vp)]),
+    ("sg_amp_plan_destroy", ct.c_int, [vp]),
+    ("sg_amp_plan_info", ct.c_int, [vp] + [ct.POINTER(ct.c_int)] * 6),
+    ("sg_amp_decode", ct.c_int, [vp, vp, ct.c_int, vp, ct.c_double, ct.c_int, ct.c_double, ct.c_int,
+                                 vp, vp, vp, vp]),
+    ("sg_amp_decode_device", ct.c_int, [vp, vp, ct.c_int, vp, ct.c_double, ct.c_int, ct.c_double,
+                                        ct.c_int, vp, vp, vp, vp, vp]),
+    ("sg_amp_apply", ct.c_int, [vp, ct.c_int, vp, ct.c_int, vp]),
+    ("sg_amp_apply_device", ct.c_int, [vp, ct.c_int, vp, ct.c_int, vp, vp]),
+    ("sg_amp_count_errors_device", ct.c_int, [vp, vp, vp, ct.c_int, ct.c_int, ct.c_int, vp, vp]),
+    ("sg_section_softmax", ct.c_int, [vp, ct.c_int, ct.c_int, ct.c_double, vp]),
+    ("sg_section_argmax", ct.c_int, [vp, ct.c_int, ct.c_int, vp]),
     ("Lxfb", ct.c_double, [dp, ct.c_long, ct.c_int]),
 ]
 

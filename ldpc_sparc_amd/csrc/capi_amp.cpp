@@ -1,0 +1,545 @@
+// C ABI of the AMP decoder: design plans (sub-sampled DCT operator tables),
+// batched decode, the design operators Ab / Az, error counting.
+#include <algorithm>
+#include <cmath>
+#include <complex>
+#include <memory>
+#include <vector>
+
+#include "amp.hpp"
+
+using cd = std::complex<double>;
+
+struct sg_amp_plan {
+    int precision = SG_F32;
+    int device = 0;
+    int ndim = 0, L = 0, M = 0, LM = 0, n = 0, Lr = 1, Lc = 1, Mr = 0, Mc = 0, nT = 0;
+    int w = 0, N2 = 0, P = 0, Q = 0, log2P = 0, log2Q = 0, npairs = 0;
+    std::vector<double> W;
+    std::vector<void *> allocs;  // every device allocation owned by the plan
+    // device tables
+    int32_t *t_row = nullptr, *t_col = nullptr, *col_ptr = nullptr, *col_t = nullptr;
+    int32_t *inmap = nullptr, *outslot = nullptr, *rp_ptr = nullptr, *rp_i = nullptr;
+    uint32_t *rp_ab = nullptr;
+    int32_t *gs_ptr = nullptr, *gs_loc = nullptr, *gs_i = nullptr;
+    void *rp_c = nullptr, *gs_c = nullptr, *twP = nullptr, *twQ = nullptr, *twHi = nullptr, *twLo = nullptr;
+    double *dW = nullptr;
+    // batch workspace (grow-only)
+    int cap_B = 0, cap_tmax = 0;
+    void *ws_beta = nullptr, *ws_y = nullptr, *ws_z = nullptr, *ws_rbuf = nullptr, *ws_buf0 = nullptr, *ws_buf1 = nullptr;
+    void *ws_io = nullptr;  // staging for host entry points
+    size_t ws_io_bytes = 0;
+    double *ws_phi = nullptr, *ws_tau = nullptr, *ws_sumsq = nullptr, *ws_err = nullptr;
+    double *ws_psi = nullptr, *ws_psi_prev = nullptr, *ws_phi_prev = nullptr, *ws_gamma = nullptr, *ws_bco = nullptr;
+    double *ws_nmse = nullptr;
+    int32_t *ws_active = nullptr, *ws_argmax = nullptr, *ws_true = nullptr, *ws_tfinal = nullptr;
+};
+
+extern "C" int sg_amp_plan_destroy(sg_amp_plan *p);
+
+namespace sg {
+
+static int ilog2(int v) {
+    int l = 0;
+    while ((1 << l) < v) ++l;
+    return l;
+}
+
+template <typename X>
+static int upload(sg_amp_plan *p, X **dst, const std::vector<X> &src) {
+    void *d = nullptr;
+    SG_HIP(hipMalloc(&d, std::max<size_t>(1, src.size() * sizeof(X))));
+    p->allocs.push_back(d);
+    if (!src.empty()) SG_HIP(hipMemcpy(d, src.data(), src.size() * sizeof(X), hipMemcpyHostToDevice));
+    *dst = (X *)d;
+    return SG_OK;
+}
+
+static int upload_cx(sg_amp_plan *p, void **dst, const std::vector<cd> &src) {
+    if (p->precision == SG_F64) {
+        std::vector<double> v(2 * src.size());
+        for (size_t i = 0; i < src.size(); ++i) { v[2 * i] = src[i].real(); v[2 * i + 1] = src[i].imag(); }
+        double *d = nullptr;
+        SG_TRY(upload(p, &d, v));
+        *dst = d;
+    } else {
+        std::vector<float> v(2 * src.size());
+        for (size_t i = 0; i < src.size(); ++i) { v[2 * i] = (float)src[i].real(); v[2 * i + 1] = (float)src[i].imag(); }
+        float *d = nullptr;
+        SG_TRY(upload(p, &d, v));
+        *dst = d;
+    }
+    return SG_OK;
+}
+
+static cd expi(double a) { return cd(std::cos(a), std::sin(a)); }
+
+// Twiddle exp(-2 pi i k / m) with exact integer reduction of k mod m.
+static cd tw(long long k, long long m) {
+    k %= m;
+    if (k < 0) k += m;
+    return expi(-2.0 * M_PI * (double)k / (double)m);
+}
+
+static int plan_free_ws(sg_amp_plan *p) {
+    void **ws[] = {&p->ws_beta, &p->ws_y, &p->ws_z, &p->ws_rbuf, &p->ws_buf0, &p->ws_buf1, &p->ws_io,
+                   (void **)&p->ws_phi, (void **)&p->ws_tau, (void **)&p->ws_sumsq, (void **)&p->ws_err,
+                   (void **)&p->ws_psi, (void **)&p->ws_psi_prev, (void **)&p->ws_phi_prev, (void **)&p->ws_gamma,
+                   (void **)&p->ws_bco, (void **)&p->ws_nmse, (void **)&p->ws_active, (void **)&p->ws_argmax,
+                   (void **)&p->ws_true, (void **)&p->ws_tfinal};
+    for (void **x : ws) {
+        if (*x) hipFree(*x);
+        *x = nullptr;
+    }
+    p->cap_B = 0;
+    p->cap_tmax = 0;
+    p->ws_io_bytes = 0;
+    return SG_OK;
+}
+
+static int ensure_ws(sg_amp_plan *p, int B, int t_max) {
+    if (B <= p->cap_B && t_max <= p->cap_tmax) return SG_OK;
+    plan_free_ws(p);
+    const size_t rs = p->precision == SG_F64 ? 8 : 4;
+    const size_t Bz = (size_t)B;
+#define SG_ALLOC(ptr, bytes) SG_HIP(hipMalloc((void **)&(ptr), std::max<size_t>(16, (bytes))))
+    SG_ALLOC(p->ws_beta, Bz * p->LM * rs);
+    SG_ALLOC(p->ws_y, Bz * p->n * rs);
+    SG_ALLOC(p->ws_z, Bz * p->n * rs);
+    SG_ALLOC(p->ws_rbuf, Bz * p->nT * p->Mr * rs);
+    SG_ALLOC(p->ws_buf0, Bz * p->nT * p->N2 * 2 * rs);
+    SG_ALLOC(p->ws_buf1, Bz * p->nT * p->N2 * 2 * rs);
+    SG_ALLOC(p->ws_phi, Bz * p->Lr * 8);
+    SG_ALLOC(p->ws_tau, Bz * p->Lc * 8);
+    SG_ALLOC(p->ws_sumsq, Bz * p->L * 8);
+    SG_ALLOC(p->ws_err, Bz * p->L * 8);
+    SG_ALLOC(p->ws_psi, Bz * p->Lc * 8);
+    SG_ALLOC(p->ws_psi_prev, Bz * p->Lc * 8);
+    SG_ALLOC(p->ws_phi_prev, Bz * p->Lr * 8);
+    SG_ALLOC(p->ws_gamma, Bz * p->Lr * 8);
+    SG_ALLOC(p->ws_bco, Bz * p->Lr * 8);
+    SG_ALLOC(p->ws_nmse, Bz * std::max(t_max, 2) * p->Lc * 8);
+    SG_ALLOC(p->ws_active, Bz * 4);
+    SG_ALLOC(p->ws_argmax, Bz * p->L * 4);
+    SG_ALLOC(p->ws_true, Bz * p->L * 4);
+    SG_ALLOC(p->ws_tfinal, Bz * 4);
+#undef SG_ALLOC
+    p->cap_B = B;
+    p->cap_tmax = std::max(t_max, 2);
+    return SG_OK;
+}
+
+template <typename T>
+static AmpTables<T> tables(const sg_amp_plan *p) {
+    AmpTables<T> tb;
+    tb.nT = p->nT; tb.w = p->w; tb.N2 = p->N2; tb.P = p->P; tb.Q = p->Q; tb.log2P = p->log2P; tb.log2Q = p->log2Q;
+    tb.npairs = p->npairs; tb.L = p->L; tb.M = p->M; tb.LM = p->LM; tb.n = p->n; tb.Lr = p->Lr; tb.Lc = p->Lc;
+    tb.Mr = p->Mr; tb.Mc = p->Mc; tb.ndim = p->ndim;
+    tb.t_row = p->t_row; tb.t_col = p->t_col; tb.col_ptr = p->col_ptr; tb.col_t = p->col_t;
+    tb.inmap = p->inmap; tb.outslot = p->outslot; tb.rp_ptr = p->rp_ptr; tb.rp_i = p->rp_i; tb.rp_ab = p->rp_ab;
+    tb.rp_c = (const cx<T> *)p->rp_c; tb.gs_ptr = p->gs_ptr; tb.gs_loc = p->gs_loc; tb.gs_i = p->gs_i;
+    tb.gs_c = (const cx<T> *)p->gs_c; tb.twP = (const cx<T> *)p->twP; tb.twQ = (const cx<T> *)p->twQ;
+    tb.twHi = (const cx<T> *)p->twHi; tb.twLo = (const cx<T> *)p->twLo;
+    return tb;
+}
+
+template <typename T>
+static AmpBufs<T> bufs(const sg_amp_plan *p, int B, const void *y) {
+    AmpBufs<T> bf;
+    bf.B = B;
+    bf.beta = (T *)p->ws_beta; bf.y = (const T *)(y ? y : p->ws_y); bf.z = (T *)p->ws_z; bf.rbuf = (T *)p->ws_rbuf;
+    bf.buf0 = (cx<T> *)p->ws_buf0; bf.buf1 = (cx<T> *)p->ws_buf1; bf.phi = p->ws_phi; bf.tau = p->ws_tau;
+    bf.active = p->ws_active; bf.sec_sumsq = p->ws_sumsq; bf.sec_err = p->ws_err; bf.sec_argmax = p->ws_argmax;
+    bf.true_idx = nullptr;
+    return bf;
+}
+
+static int build_plan(int ndim, const double *W, int Lr_in, int Lc_in, int L, int M, int n, const uint32_t *order0,
+                      const uint32_t *order1, int precision, sg_amp_plan **out) {
+    SG_CHECK_ARG(out && W && order0 && order1, "null argument");
+    SG_CHECK_ARG(ndim >= 0 && ndim <= 2, "W.ndim must be 0, 1 or 2");
+    SG_CHECK_ARG(precision == SG_F32 || precision == SG_F64, "precision must be SG_F32 or SG_F64");
+    SG_CHECK_ARG(L > 0 && M > 0 && n > 0 && (M & (M - 1)) == 0, "bad (L, M, n)");
+    SG_TRY(ensure_device());
+    int Lr = 1, Lc = 1;
+    if (ndim == 1) Lc = Lc_in;
+    if (ndim == 2) { Lr = Lr_in; Lc = Lc_in; }
+    SG_CHECK_ARG(Lr >= 1 && Lc >= 1, "bad base-matrix shape");
+    const long long LM = (long long)L * M;
+    SG_CHECK_ARG(LM < (1LL << 30), "L*M too large");
+    SG_CHECK_ARG(L % Lc == 0, "Lc must divide L");
+    SG_CHECK_ARG(ndim != 2 || n % Lr == 0, "Lr must divide n");
+    const int Mr = (ndim == 2) ? n / Lr : n;
+    const int Mc = (int)(LM / Lc);
+    int w = 1;
+    while (w < std::max(Mr + 1, Mc + 1)) w <<= 1;  // sparc.py:744
+    SG_CHECK_ARG(w >= 16 && w <= (1 << 23), "transform size w=%d outside [16, 2^23]", w);
+    std::unique_ptr<sg_amp_plan> p(new sg_amp_plan());
+    hipGetDevice(&p->device);
+    p->precision = precision; p->ndim = ndim; p->L = L; p->M = M; p->LM = (int)LM; p->n = n;
+    p->Lr = Lr; p->Lc = Lc; p->Mr = Mr; p->Mc = Mc; p->w = w; p->N2 = w / 2;
+    const int lg = ilog2(p->N2);
+    p->log2P = lg / 2; p->log2Q = lg - p->log2P;
+    p->P = 1 << p->log2P; p->Q = 1 << p->log2Q;
+    p->npairs = p->P / 2 + 1;
+    p->W.assign(W, W + (ndim == 0 ? 1 : (size_t)Lr * Lc));
+    // transforms = nonzero blocks in row-major order (sparc.py:758-771)
+    std::vector<int32_t> t_row, t_col;
+    std::vector<double> t_scale;
+    for (int r = 0; r < Lr; ++r)
+        for (int c = 0; c < Lc; ++c) {
+            const double wv = (ndim == 0) ? p->W[0] : p->W[(size_t)r * Lc + c];
+            if (wv != 0.0) {
+                t_row.push_back(r); t_col.push_back(c);
+                t_scale.push_back(std::sqrt(wv / L));  // np.sqrt(W/L)
+            }
+        }
+    p->nT = (int)t_row.size();
+    SG_CHECK_ARG(p->nT > 0, "base matrix is all zero");
+    std::vector<int32_t> col_ptr(Lc + 1, 0), col_t;
+    for (int c = 0; c < Lc; ++c) {
+        for (int t = 0; t < p->nT; ++t)
+            if (t_col[t] == c) col_t.push_back(t);
+        col_ptr[c + 1] = (int32_t)col_t.size();
+    }
+    const int N = w, N2 = p->N2, P = p->P, Q = p->Q, np1 = p->npairs + 1;
+    auto slot_of = [&](long long pos) -> long long {  // w-space slot of position pos
+        return (pos % 2 == 0) ? pos / 2 : (long long)N - 1 - (pos - 1) / 2;
+    };
+    auto pair_of = [&](long long k) -> int {  // row pair of an N2-index
+        const int row = (int)(k % P);
+        return row <= P / 2 ? row : P - row;
+    };
+    auto local_of = [&](long long k) -> uint32_t {  // LDS index of N2-index k inside its pair's two rows
+        const int row = (int)(k % P);
+        const int pr = row <= P / 2 ? row : P - row;
+        const int half = (row == pr) ? 0 : 1;
+        return (uint32_t)(half * Q + (int)(k / P));
+    };
+    std::vector<int32_t> inmap((size_t)p->nT * N, -1), outslot((size_t)p->nT * Mc);
+    std::vector<int32_t> rp_ptr((size_t)p->nT * np1), rp_i;
+    std::vector<uint32_t> rp_ab;
+    std::vector<cd> rp_c;
+    std::vector<int32_t> gs_ptr((size_t)p->nT * np1), gs_loc, gs_i;
+    std::vector<cd> gs_c;
+    const double sqrt2 = std::sqrt(2.0);
+    for (int t = 0; t < p->nT; ++t) {
+        const uint32_t *o0 = order0 + (size_t)t * Mr, *o1 = order1 + (size_t)t * Mc;
+        int32_t *im = inmap.data() + (size_t)t * N;
+        for (int j = 0; j < Mc; ++j) {
+            const long long pos = o1[j];
+            SG_CHECK_ARG(pos >= 1 && pos < N, "order1 entry %lld outside [1, w)", pos);
+            const long long sl = slot_of(pos);
+            SG_CHECK_ARG(im[sl] < 0, "order1 has a repeated position");
+            im[sl] = j;
+            outslot[(size_t)t * Mc + j] = (int32_t)sl;
+        }
+        const double sc = t_scale[t];
+        // ---- forward outputs X[k], k = order0[i], grouped by row pair
+        std::vector<std::vector<int>> by_pair(p->npairs);
+        std::vector<int> seen0(N, 0);
+        for (int i = 0; i < Mr; ++i) {
+            const long long k = o0[i];
+            SG_CHECK_ARG(k >= 1 && k < N, "order0 entry %lld outside [1, w)", k);
+            SG_CHECK_ARG(!seen0[k], "order0 has a repeated position");
+            seen0[k] = 1;
+            const long long kk = (k <= N2) ? k : N - k;
+            by_pair[pair_of(kk % N2)].push_back(i);
+        }
+        for (int pr = 0; pr < p->npairs; ++pr) {
+            rp_ptr[(size_t)t * np1 + pr] = (int32_t)rp_i.size();
+            for (int i : by_pair[pr]) {
+                const long long k = o0[i];
+                const long long kk = (k <= N2) ? k : N - k;
+                const long long a = kk % N2, b = (N2 - kk) % N2;
+                const cd e = (k <= N2) ? expi(-M_PI * (double)k / (2.0 * N)) : expi(M_PI * (double)k / (2.0 * N));
+                const cd wk = tw(kk, N);
+                const cd I(0, 1);
+                const cd c1 = e * (0.5 - 0.5 * I * wk) * (sqrt2 * sc);
+                const cd c2 = e * (0.5 + 0.5 * I * wk) * (sqrt2 * sc);
+                rp_i.push_back(i);
+                rp_ab.push_back(local_of(a) | (local_of(b) << 16));
+                rp_c.push_back(c1);
+                rp_c.push_back(c2);
+            }
+        }
+        rp_ptr[(size_t)t * np1 + p->npairs] = (int32_t)rp_i.size();
+        // ---- inverse inputs: G[k] = A_k y[k] - i A_k y[N-k] + C_k y[N2+k] - i C_k y[N2-k]
+        std::vector<std::vector<std::pair<int, cd>>> gcon(N2);
+        const cd I(0, 1);
+        auto Ak = [&](long long k) { return expi(M_PI * (double)k / (2.0 * N)) * (1.0 + I * tw(-k, N)); };
+        auto Ck = [&](long long k) { return expi(M_PI * (double)(k + N2) / (2.0 * N)) * (1.0 - I * tw(-k, N)); };
+        const double gsc = sc / sqrt2;  // sqrt(2 W/L) * (1/2)
+        for (int i = 0; i < Mr; ++i) {
+            const long long q = o0[i];
+            if (q < N2) {
+                gcon[q].push_back({i, Ak(q) * gsc});
+                gcon[N2 - q].push_back({i, -I * Ck(N2 - q) * gsc});
+            } else if (q > N2) {
+                gcon[N - q].push_back({i, -I * Ak(N - q) * gsc});
+                gcon[q - N2].push_back({i, Ck(q - N2) * gsc});
+            } else {
+                gcon[0].push_back({i, Ck(0) * (1.0 - I) * gsc});
+            }
+        }
+        std::vector<std::vector<int>> slots_by_pair(p->npairs);
+        for (int k = 0; k < N2; ++k)
+            if (!gcon[k].empty()) slots_by_pair[pair_of(k)].push_back(k);
+        for (int pr = 0; pr < p->npairs; ++pr) {
+            gs_ptr[(size_t)t * np1 + pr] = (int32_t)gs_loc.size();
+            for (int k : slots_by_pair[pr]) {
+                SG_CHECK_ARG(gcon[k].size() <= 4, "internal: >4 contributions to one G slot");
+                gs_loc.push_back((int32_t)local_of(k));
+                for (int q = 0; q < 4; ++q) {
+                    if (q < (int)gcon[k].size()) { gs_i.push_back(gcon[k][q].first); gs_c.push_back(gcon[k][q].second); }
+                    else { gs_i.push_back(-1); gs_c.push_back(cd(0, 0)); }
+                }
+            }
+        }
+        gs_ptr[(size_t)t * np1 + p->npairs] = (int32_t)gs_loc.size();
+    }
+    std::vector<cd> twP(P), twQ(Q), twHi((N2 + 1023) / 1024), twLo(std::min(N2, 1024));
+    for (int i = 0; i < P; ++i) twP[i] = tw(i, P);
+    for (int i = 0; i < Q; ++i) twQ[i] = tw(i, Q);
+    for (size_t i = 0; i < twHi.size(); ++i) twHi[i] = tw((long long)i * 1024, N2);
+    for (size_t i = 0; i < twLo.size(); ++i) twLo[i] = tw((long long)i, N2);
+    std::vector<double> Wd = p->W;
+    sg_amp_plan *pp = p.release();
+    int rc = [&]() -> int {
+    SG_TRY(upload(pp, &pp->t_row, t_row));
+    SG_TRY(upload(pp, &pp->t_col, t_col));
+    SG_TRY(upload(pp, &pp->col_ptr, col_ptr));
+    SG_TRY(upload(pp, &pp->col_t, col_t));
+    SG_TRY(upload(pp, &pp->inmap, inmap));
+    SG_TRY(upload(pp, &pp->outslot, outslot));
+    SG_TRY(upload(pp, &pp->rp_ptr, rp_ptr));
+    SG_TRY(upload(pp, &pp->rp_i, rp_i));
+    SG_TRY(upload(pp, &pp->rp_ab, rp_ab));
+    SG_TRY(upload_cx(pp, &pp->rp_c, rp_c));
+    SG_TRY(upload(pp, &pp->gs_ptr, gs_ptr));
+    SG_TRY(upload(pp, &pp->gs_loc, gs_loc));
+    SG_TRY(upload(pp, &pp->gs_i, gs_i));
+    SG_TRY(upload_cx(pp, &pp->gs_c, gs_c));
+    SG_TRY(upload_cx(pp, &pp->twP, twP));
+    SG_TRY(upload_cx(pp, &pp->twQ, twQ));
+    SG_TRY(upload_cx(pp, &pp->twHi, twHi));
+    SG_TRY(upload_cx(pp, &pp->twLo, twLo));
+    SG_TRY(upload(pp, &pp->dW, Wd));
+    return SG_OK;
+    }();
+    if (rc != SG_OK) {
+        sg_amp_plan_destroy(pp);
+        return rc;
+    }
+    *out = pp;
+    return SG_OK;
+}
+
+template <typename T>
+static int decode_impl(sg_amp_plan *p, const void *d_y, int B, const int32_t *d_true, double awgn_var, int t_max,
+                       double rtol, int phi_method, int32_t *d_map, int32_t *d_tfinal, double *d_nmse, double *d_psi,
+                       hipStream_t s) {
+    SG_TRY(ensure_ws(p, B, t_max));
+    AmpTables<T> tb = tables<T>(p);
+    AmpBufs<T> bf = bufs<T>(p, B, d_y);
+    bf.true_idx = d_true;
+    AmpScalars sc;
+    sc.psi = p->ws_psi; sc.psi_prev = p->ws_psi_prev; sc.phi_prev = p->ws_phi_prev; sc.gamma = p->ws_gamma;
+    sc.bcoef = p->ws_bco; sc.nmse = p->ws_nmse; sc.t_final = p->ws_tfinal;
+    AmpParams pr;
+    pr.W = p->dW; pr.awgn_var = awgn_var; pr.rtol = rtol;
+    pr.atol = 2e-15;  // 2*np.finfo(float).resolution, sparc.py:916
+    pr.phi_method = phi_method; pr.t_max = t_max;
+    const size_t rs = sizeof(T);
+    SG_HIP(hipMemsetAsync(p->ws_beta, 0, (size_t)B * p->LM * rs, s));
+    SG_TRY(amp_launch_control<T>(tb, bf, sc, pr, 2, 0, s));
+    std::vector<int32_t> act(B);
+    for (int t = 0; t < t_max - 1; ++t) {
+        if (t > 0) SG_TRY(amp_launch_ab<T>(tb, bf, s));
+        SG_TRY(amp_launch_control<T>(tb, bf, sc, pr, 0, t, s));
+        SG_TRY(amp_launch_az<T>(tb, bf, s));
+        SG_TRY(amp_launch_eta<T>(tb, bf, s));
+        SG_TRY(amp_launch_control<T>(tb, bf, sc, pr, 1, t, s));
+        if (t % 4 == 3 && t + 1 < t_max - 1) {  // skip the remaining launches once every codeword stopped
+            SG_HIP(hipMemcpyAsync(act.data(), p->ws_active, sizeof(int32_t) * B, hipMemcpyDeviceToHost, s));
+            SG_HIP(hipStreamSynchronize(s));
+            bool any = false;
+            for (int b = 0; b < B; ++b) any |= act[b] != 0;
+            if (!any) break;
+        }
+    }
+    if (d_map) SG_HIP(hipMemcpyAsync(d_map, p->ws_argmax, sizeof(int32_t) * B * p->L, hipMemcpyDeviceToDevice, s));
+    if (d_tfinal) SG_HIP(hipMemcpyAsync(d_tfinal, p->ws_tfinal, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
+    if (d_nmse) SG_HIP(hipMemcpyAsync(d_nmse, p->ws_nmse, sizeof(double) * B * t_max * p->Lc, hipMemcpyDeviceToDevice, s));
+    if (d_psi) SG_HIP(hipMemcpyAsync(d_psi, p->ws_psi, sizeof(double) * B * p->Lc, hipMemcpyDeviceToDevice, s));
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
+template <typename T>
+static int apply_impl(sg_amp_plan *p, int transpose, const void *d_in, int in_is_double, int B, void *d_out,
+                      int out_double, hipStream_t s) {
+    SG_TRY(ensure_ws(p, B, 2));
+    AmpTables<T> tb = tables<T>(p);
+    AmpBufs<T> bf = bufs<T>(p, B, nullptr);
+    // all codewords active
+    std::vector<int32_t> ones(B, 1);
+    SG_HIP(hipMemcpyAsync(p->ws_active, ones.data(), sizeof(int32_t) * B, hipMemcpyHostToDevice, s));
+    if (!transpose) {
+        SG_TRY(amp_launch_cast<T>(d_in, in_is_double, (T *)p->ws_beta, (size_t)B * p->LM, s));
+        SG_TRY(amp_launch_ab<T>(tb, bf, s));
+        T *out = out_double ? (T *)p->ws_z : (T *)d_out;
+        SG_TRY(amp_launch_rowsum<T>(tb, bf, out, s));
+        if (out_double) SG_TRY(amp_launch_uncast<T>(out, (double *)d_out, (size_t)B * p->n, s));
+    } else {
+        SG_TRY(amp_launch_cast<T>(d_in, in_is_double, (T *)p->ws_z, (size_t)B * p->n, s));
+        std::vector<double> ph((size_t)B * p->Lr, 1.0);
+        SG_HIP(hipMemcpyAsync(p->ws_phi, ph.data(), sizeof(double) * ph.size(), hipMemcpyHostToDevice, s));
+        SG_TRY(amp_launch_az<T>(tb, bf, s));
+        T *out = out_double ? (T *)p->ws_beta : (T *)d_out;
+        SG_TRY(amp_launch_colgather<T>(tb, bf, out, s));
+        if (out_double) SG_TRY(amp_launch_uncast<T>(out, (double *)d_out, (size_t)B * p->LM, s));
+    }
+    SG_HIP(hipStreamSynchronize(s));
+    return SG_OK;
+}
+
+static int ensure_io(sg_amp_plan *p, size_t bytes) {
+    if (bytes <= p->ws_io_bytes) return SG_OK;
+    if (p->ws_io) hipFree(p->ws_io);
+    p->ws_io = nullptr;
+    p->ws_io_bytes = 0;
+    SG_HIP(hipMalloc(&p->ws_io, bytes));
+    p->ws_io_bytes = bytes;
+    return SG_OK;
+}
+
+}  // namespace sg
+
+using namespace sg;
+
+extern "C" {
+
+int sg_amp_plan_create(int ndim, const double *W, int Lr, int Lc, int L, int M, int n, const uint32_t *order0,
+                       const uint32_t *order1, int precision, sg_amp_plan **out) {
+    return build_plan(ndim, W, Lr, Lc, L, M, n, order0, order1, precision, out);
+}
+
+int sg_amp_plan_destroy(sg_amp_plan *p) {
+    if (!p) return SG_OK;
+    plan_free_ws(p);
+    for (void *a : p->allocs) hipFree(a);
+    delete p;
+    return SG_OK;
+}
+
+int sg_amp_plan_info(const sg_amp_plan *p, int *w, int *nT, int *Mr, int *Mc, int *P, int *Q) {
+    SG_CHECK_ARG(p, "plan is NULL");
+    if (w) *w = p->w;
+    if (nT) *nT = p->nT;
+    if (Mr) *Mr = p->Mr;
+    if (Mc) *Mc = p->Mc;
+    if (P) *P = p->P;
+    if (Q) *Q = p->Q;
+    return SG_OK;
+}
+
+int sg_amp_decode_device(sg_amp_plan *p, const void *d_y, int B, const int32_t *d_true_idx, double awgn_var,
+                         int t_max, double rtol, int phi_method, int32_t *d_map_idx, int32_t *d_t_final,
+                         double *d_nmse, double *d_psi, void *stream) {
+    SG_CHECK_ARG(p, "plan is NULL");
+    SG_CHECK_ARG(t_max > 1, "t_max must be > 1 (sparc.py:168)");
+    SG_CHECK_ARG(rtol > 0 && rtol < 1, "rtol must be in (0, 1)");
+    SG_CHECK_ARG(phi_method == 1 || phi_method == 2, "phi_est_method must be 1 or 2");
+    SG_CHECK_ARG(awgn_var >= 0, "awgn_var must be >= 0");
+    SG_CHECK_ARG(B >= 0, "negative batch");
+    if (B == 0) return SG_OK;
+    SG_CHECK_ARG(d_y, "d_y is NULL");
+    SG_TRY(ensure_device());
+    SG_HIP(hipSetDevice(p->device));
+    hipStream_t s = pick_stream(stream);
+    if (p->precision == SG_F64)
+        return decode_impl<double>(p, d_y, B, d_true_idx, awgn_var, t_max, rtol, phi_method, d_map_idx, d_t_final,
+                                   d_nmse, d_psi, s);
+    return decode_impl<float>(p, d_y, B, d_true_idx, awgn_var, t_max, rtol, phi_method, d_map_idx, d_t_final, d_nmse,
+                              d_psi, s);
+}
+
+int sg_amp_decode(sg_amp_plan *p, const double *y, int B, const int32_t *true_idx, double awgn_var, int t_max,
+                  double rtol, int phi_method, int32_t *map_idx, int32_t *t_final, double *nmse, double *psi) {
+    SG_CHECK_ARG(p, "plan is NULL");
+    SG_CHECK_ARG(B >= 0, "negative batch");
+    if (B == 0) return SG_OK;
+    SG_CHECK_ARG(y && map_idx && t_final && nmse && psi, "null host buffer");
+    SG_CHECK_ARG(t_max > 1, "t_max must be > 1 (sparc.py:168)");
+    SG_TRY(ensure_device());
+    SG_HIP(hipSetDevice(p->device));
+    hipStream_t s = lib_stream();
+    SG_TRY(ensure_ws(p, B, t_max));
+    const size_t ny = (size_t)B * p->n;
+    SG_TRY(ensure_io(p, ny * sizeof(double)));
+    SG_HIP(hipMemcpyAsync(p->ws_io, y, ny * sizeof(double), hipMemcpyHostToDevice, s));
+    int r;
+    if (p->precision == SG_F64) {
+        r = amp_launch_cast<double>(p->ws_io, 1, (double *)p->ws_y, ny, s);
+    } else {
+        r = amp_launch_cast<float>(p->ws_io, 1, (float *)p->ws_y, ny, s);
+    }
+    SG_TRY(r);
+    const int32_t *d_true = nullptr;
+    if (true_idx) {
+        SG_HIP(hipMemcpyAsync(p->ws_true, true_idx, sizeof(int32_t) * B * p->L, hipMemcpyHostToDevice, s));
+        d_true = p->ws_true;
+    }
+    if (p->precision == SG_F64)
+        r = decode_impl<double>(p, p->ws_y, B, d_true, awgn_var, t_max, rtol, phi_method, nullptr, nullptr, nullptr,
+                                nullptr, s);
+    else
+        r = decode_impl<float>(p, p->ws_y, B, d_true, awgn_var, t_max, rtol, phi_method, nullptr, nullptr, nullptr,
+                               nullptr, s);
+    SG_TRY(r);
+    SG_HIP(hipMemcpyAsync(map_idx, p->ws_argmax, sizeof(int32_t) * B * p->L, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipMemcpyAsync(t_final, p->ws_tfinal, sizeof(int32_t) * B, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipMemcpyAsync(nmse, p->ws_nmse, sizeof(double) * B * t_max * p->Lc, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipMemcpyAsync(psi, p->ws_psi, sizeof(double) * B * p->Lc, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    return SG_OK;
+}
+
+int sg_amp_apply(sg_amp_plan *p, int transpose, const double *in, int B, double *out) {
+    SG_CHECK_ARG(p && in && out, "null argument");
+    SG_CHECK_ARG(B >= 0, "negative batch");
+    if (B == 0) return SG_OK;
+    SG_TRY(ensure_device());
+    SG_HIP(hipSetDevice(p->device));
+    hipStream_t s = lib_stream();
+    const size_t nin = (size_t)B * (transpose ? p->n : p->LM), nout = (size_t)B * (transpose ? p->LM : p->n);
+    SG_TRY(ensure_ws(p, B, 2));
+    SG_TRY(ensure_io(p, (nin + nout) * sizeof(double)));
+    double *din = (double *)p->ws_io, *dout = din + nin;
+    SG_HIP(hipMemcpyAsync(din, in, nin * sizeof(double), hipMemcpyHostToDevice, s));
+    int r = (p->precision == SG_F64) ? apply_impl<double>(p, transpose, din, 1, B, dout, 1, s)
+                                     : apply_impl<float>(p, transpose, din, 1, B, dout, 1, s);
+    SG_TRY(r);
+    SG_HIP(hipMemcpyAsync(out, dout, nout * sizeof(double), hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    return SG_OK;
+}
+
+int sg_amp_apply_device(sg_amp_plan *p, int transpose, const void *d_in, int B, void *d_out, void *stream) {
+    SG_CHECK_ARG(p && d_in && d_out, "null argument");
+    if (B <= 0) return SG_OK;
+    SG_TRY(ensure_device());
+    hipStream_t s = pick_stream(stream);
+    if (p->precision == SG_F64) return apply_impl<double>(p, transpose, d_in, 1, B, d_out, 0, s);
+    return apply_impl<float>(p, transpose, d_in, 0, B, d_out, 0, s);
+}
+
+int sg_amp_count_errors_device(const int32_t *d_map_idx, const int32_t *d_true_idx, const int32_t *d_t_final, int B,
+                               int L, int logM, int64_t *d_counts, void *stream) {
+    SG_CHECK_ARG(d_map_idx && d_true_idx && d_t_final && d_counts, "null device buffer");
+    SG_TRY(ensure_device());
+    return amp_launch_count(d_map_idx, d_true_idx, d_t_final, B, L, logM, d_counts, pick_stream(stream));
+}
+
+}  // extern "C"

@@ -1,0 +1,155 @@
+// Workgroup-cooperative complex FFTs in LDS for gfx950 (device code).
+//
+// Used by the sub-sampled DCT design operator (amp_dct.hip): the length-w
+// DCT-II/III of the reference (sparc.py:687-699, scipy.fftpack dct/idct,
+// norm='ortho') is evaluated as a length-w/2 complex FFT (Makhoul packing),
+// itself split four-step into P-point column FFTs and Q-point row FFTs.  Each
+// of those short FFTs runs here: a Stockham autosort radix-8/4/2 schedule in
+// which every thread keeps EPT complex values in registers; one stage = load
+// R inputs per butterfly from LDS, twiddle, R-point DFT in registers, barrier,
+// store R outputs, barrier.  Twiddles come from a per-size table
+// tw[i] = exp(-2*pi*i*i/n), i < n, computed in double on the host.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace sg {
+
+template <typename T>
+struct cx {
+    T x, y;
+};
+
+template <typename T>
+__device__ __forceinline__ cx<T> cadd(cx<T> a, cx<T> b) { return {a.x + b.x, a.y + b.y}; }
+template <typename T>
+__device__ __forceinline__ cx<T> csub(cx<T> a, cx<T> b) { return {a.x - b.x, a.y - b.y}; }
+template <typename T>
+__device__ __forceinline__ cx<T> cmul(cx<T> a, cx<T> b) {
+    return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x};
+}
+template <typename T>
+__device__ __forceinline__ cx<T> cconj(cx<T> a) { return {a.x, -a.y}; }
+// multiply by -i (forward) or +i (inverse)
+template <typename T, bool INV>
+__device__ __forceinline__ cx<T> mul_mi(cx<T> a) {
+    return INV ? cx<T>{-a.y, a.x} : cx<T>{a.y, -a.x};
+}
+
+template <typename T, bool INV>
+__device__ __forceinline__ void dft2(cx<T> *a) {
+    const cx<T> t = a[0];
+    a[0] = cadd(t, a[1]);
+    a[1] = csub(t, a[1]);
+}
+
+template <typename T, bool INV>
+__device__ __forceinline__ void dft4(cx<T> *a) {
+    const cx<T> t0 = cadd(a[0], a[2]), t1 = csub(a[0], a[2]);
+    const cx<T> t2 = cadd(a[1], a[3]), t3 = mul_mi<T, INV>(csub(a[1], a[3]));
+    a[0] = cadd(t0, t2);
+    a[2] = csub(t0, t2);
+    a[1] = cadd(t1, t3);
+    a[3] = csub(t1, t3);
+}
+
+template <typename T, bool INV>
+__device__ __forceinline__ void dft8(cx<T> *a) {
+    const T r = T(0.70710678118654752440084436210484903928);
+    cx<T> b[4], c[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        b[k] = cadd(a[k], a[k + 4]);
+        c[k] = csub(a[k], a[k + 4]);
+    }
+    // c[k] *= w8^k (forward w8 = e^{-i pi/4}; inverse conjugated)
+    c[1] = INV ? cx<T>{(c[1].x - c[1].y) * r, (c[1].x + c[1].y) * r}
+               : cx<T>{(c[1].x + c[1].y) * r, (c[1].y - c[1].x) * r};
+    c[2] = mul_mi<T, INV>(c[2]);
+    c[3] = INV ? cx<T>{-(c[3].x + c[3].y) * r, (c[3].x - c[3].y) * r}
+               : cx<T>{(c[3].y - c[3].x) * r, -(c[3].x + c[3].y) * r};
+    dft4<T, INV>(b);
+    dft4<T, INV>(c);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        a[2 * m] = b[m];
+        a[2 * m + 1] = c[m];
+    }
+}
+
+template <typename T, bool INV, int R>
+__device__ __forceinline__ void dftR(cx<T> *a) {
+    if (R == 2) dft2<T, INV>(a);
+    else if (R == 4) dft4<T, INV>(a);
+    else dft8<T, INV>(a);
+}
+
+// Sequence layout in LDS: element e of sequence s lives at d[s*ss + e*es].
+// SEQ_FAST: consecutive butterflies walk sequences first (use when sequences
+// are the unit-stride dimension, e.g. column tiles); otherwise they walk the
+// elements of one sequence first.
+template <typename T, bool INV, int R, int EPT, bool SEQ_FAST>
+__device__ __forceinline__ void stockham_stage(cx<T> *d, int n, int nseq, int es, int ss, int Ns,
+                                               const cx<T> *__restrict__ tw, int tid, int nthr) {
+    constexpr int NB = EPT / R;  // butterflies per thread
+    const int nbf = n / R;       // butterflies per sequence
+    cx<T> v[EPT];
+    int base_out[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        const int b = tid + i * nthr;
+        const int s = SEQ_FAST ? (b % nseq) : (b / nbf);
+        const int j = SEQ_FAST ? (b / nseq) : (b % nbf);
+        const int k = j % Ns;
+        cx<T> *ds = d + s * ss;
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[i * R + r] = ds[(j + r * nbf) * es];
+        if (Ns > 1) {
+            const int step = n / (Ns * R);  // tw index of w_{Ns R}^{r k}
+#pragma unroll
+            for (int r = 1; r < R; ++r) {
+                cx<T> w = tw[r * k * step];
+                if (INV) w.y = -w.y;
+                v[i * R + r] = cmul(v[i * R + r], w);
+            }
+        }
+        dftR<T, INV, R>(&v[i * R]);
+        base_out[i] = s * ss + ((j - k) * R + k) * es;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) d[base_out[i] + r * Ns * es] = v[i * R + r];
+    }
+    __syncthreads();
+}
+
+// Full FFT of nseq sequences of length n = 2^log2n in LDS, nthr*EPT == n*nseq.
+// Radix plan: as many radix-8 stages as possible, the remainder as one radix-4
+// or two radix-4 (never a radix-2 unless n == 2).
+template <typename T, bool INV, int EPT, bool SEQ_FAST>
+__device__ void lds_fft(cx<T> *d, int log2n, int nseq, int es, int ss, const cx<T> *__restrict__ tw, int tid,
+                        int nthr) {
+    const int n = 1 << log2n;
+    int a8 = log2n / 3, rem = log2n % 3, n4 = 0, n2 = 0;
+    if (rem == 2) n4 = 1;
+    else if (rem == 1) {
+        if (a8 >= 1) { a8 -= 1; n4 = 2; }
+        else n2 = 1;
+    }
+    int Ns = 1;
+    for (int s = 0; s < n2; ++s) {
+        stockham_stage<T, INV, 2, EPT, SEQ_FAST>(d, n, nseq, es, ss, Ns, tw, tid, nthr);
+        Ns *= 2;
+    }
+    for (int s = 0; s < n4; ++s) {
+        stockham_stage<T, INV, 4, EPT, SEQ_FAST>(d, n, nseq, es, ss, Ns, tw, tid, nthr);
+        Ns *= 4;
+    }
+    for (int s = 0; s < a8; ++s) {
+        stockham_stage<T, INV, 8, EPT, SEQ_FAST>(d, n, nseq, es, ss, Ns, tw, tid, nthr);
+        Ns *= 8;
+    }
+}
+
+}  // namespace sg

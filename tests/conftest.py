@@ -28,3 +28,15 @@ def oracle_built():
         subprocess.run(["make", "-C", os.path.join(REPO, "oracle")], check=True,
                        capture_output=True)
     return lib
+
+
+@pytest.fixture(scope="session")
+def sparc_golden():
+    import numpy as np
+    return np.load(os.path.join(REPO, "tests", "golden", "sparc_golden.npz"))
+
+
+@pytest.fixture(scope="session")
+def sophie_golden():
+    import numpy as np
+    return np.load(os.path.join(REPO, "tests", "golden", "sophie_golden.npz"))

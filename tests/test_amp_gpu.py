@@ -1,0 +1,204 @@
+"""GPU parity tests of the SPARC AMP engine (amp_dct.hip) through the C ABI.
+
+Bars (stated tolerances):
+  * design operators Ab / Az: double plan within 1e-12 of the reference
+    operator (relative to the output's max magnitude), float plan within 2e-6;
+  * double-precision decode: identical t_final and MAP decision as the
+    reference on every golden seed, NMSE per iteration within 1e-9;
+  * float decode: identical MAP decision on seeds the reference decodes
+    (BER 0), t_final within +-2, NMSE per iteration within 1e-3 absolute for
+    the first iterations;
+  * full size (L=1024, M=512, w=2^20): operators as above; R=1.3 codewords
+    decode with BER 0; NMSE trajectory tracks the CPU restatement.
+"""
+import numpy as np
+import pytest
+
+from ldpc_sparc_amd import _native, sparc, sparc_sim
+from oracle import sparc_ref
+from sparc_cases import SPARC_CASES, all_seeds, design
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300)
+
+
+@pytest.mark.parametrize("name,cp,dp,var,si", [c for c in all_seeds() if c[4] == 0])
+def test_operators_vs_reference(sparc_golden, name, cp, dp, var, si):
+    W, L, M, n, o0, o1 = design(sparc_golden, name, si, cp, var)
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    Ab, Az = sparc_ref.dct_operators(W, L, M, n, o0, o1)
+    rng = np.random.default_rng(1)
+    X = rng.standard_normal((3, L * M))
+    Y = rng.standard_normal((3, n))
+    for prec, tol in ((_native.SG_F64, 1e-12), (_native.SG_F32, 2e-6)):
+        gx = op.apply(X, False, prec)
+        gy = op.apply(Y, True, prec)
+        for b in range(3):
+            assert _rel(gx[b], Ab(X[b])) < tol, (name, prec)
+            assert _rel(gy[b], Az(Y[b])) < tol, (name, prec)
+
+
+@pytest.mark.parametrize("w_exp,Mr", [(4, 5), (5, 12), (7, 40), (10, 300), (13, 1000), (16, 6000)])
+def test_operator_sizes(w_exp, Mr):
+    """Transform sizes from w=16 to 2^16 with random orders (odd P/Q splits)."""
+    w = 2 ** w_exp
+    Mc = w // 2 + 3 if w > 16 else 9
+    L, M = Mc, 1
+    rng = np.random.RandomState(w_exp)
+    idx0 = np.arange(1, w, dtype=np.uint32); rng.shuffle(idx0)
+    idx1 = np.arange(1, w, dtype=np.uint32); rng.shuffle(idx1)
+    o0, o1 = idx0[:Mr], idx1[:Mc]
+    W = np.array(3.0)
+    op = sparc.DesignOperator(W, L, M, Mr, o0, o1)
+    assert op.w == w
+    Ab, Az = sparc_ref.dct_operators(W, L, M, Mr, o0, o1)
+    x = rng.standard_normal(L * M)
+    y = rng.standard_normal(Mr)
+    assert _rel(op.Ab(x), Ab(x)) < 1e-12
+    assert _rel(op.Az(y), Az(y)) < 1e-12
+
+
+@pytest.mark.parametrize("name,cp,dp,var,si", list(all_seeds()))
+def test_decode_f64_matches_reference(sparc_golden, name, cp, dp, var, si):
+    key = f"{name}_s{si}"
+    W, L, M, n, o0, o1 = design(sparc_golden, name, si, cp, var)
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    dp = dict(dp)
+    sparc.check_decode_params(dp)
+    true = sparc.bin_arr_2_msg_vector(sparc_golden[key + "_bits"], M).reshape(L, M).argmax(1)
+    mi, tf, nmse, psi = sparc.amp_decode_batch(sparc_golden[key + "_y"][None], op, var, dp['t_max'],
+                                               dp['rtol'], dp['phi_est_method'], true[None])
+    assert tf[0] == int(sparc_golden[key + "_t_final"]), key
+    assert np.array_equal(mi[0], sparc_golden[key + "_map"]), key
+    ref_nmse = sparc_golden[key + "_nmse"]
+    np.testing.assert_allclose(nmse[0].reshape(ref_nmse.shape), ref_nmse, rtol=0, atol=1e-9, err_msg=key)
+
+
+@pytest.mark.parametrize("name,cp,dp,var,si", list(all_seeds()))
+def test_sparc_sim_dropin_matches_reference(sparc_golden, name, cp, dp, var, si):
+    """sparc_sim (the reference's call surface) end to end on the GPU."""
+    key = f"{name}_s{si}"
+    seed = [int(v) for v in sparc_golden[key + "_seed"]]
+    res = sparc_sim.sparc_sim(dict(cp), dict(dp), var, seed)
+    assert res['ber'] == float(sparc_golden[key + "_sim_ber"])
+    assert res['ser'] == float(sparc_golden[key + "_sim_ser"])
+    assert res['t_final'] == int(sparc_golden[key + "_sim_t"])
+    assert res['detect'] == float(sparc_golden[key + "_sim_detect"])
+    assert res['num_of_sec_errs'] == int(sparc_golden[key + "_sim_nsec"])
+    assert np.array_equal(res['loc_of_sec_errs'], sparc_golden[key + "_sim_locs"])
+
+
+@pytest.mark.parametrize("name,cp,dp,var,si", list(all_seeds()))
+def test_decode_f32_tolerance(sparc_golden, name, cp, dp, var, si):
+    key = f"{name}_s{si}"
+    W, L, M, n, o0, o1 = design(sparc_golden, name, si, cp, var)
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    dp = dict(dp)
+    sparc.check_decode_params(dp)
+    true = sparc.bin_arr_2_msg_vector(sparc_golden[key + "_bits"], M).reshape(L, M).argmax(1)
+    mi, tf, nmse, psi = sparc.amp_decode_batch(sparc_golden[key + "_y"][None], op, var, dp['t_max'],
+                                               dp['rtol'], dp['phi_est_method'], true[None],
+                                               precision=_native.SG_F32)
+    ref_map = sparc_golden[key + "_map"]
+    ref_nmse = sparc_golden[key + "_nmse"].reshape(nmse[0].shape)
+    decoded = float(sparc_golden[key + "_sim_ber"]) == 0.0
+    if decoded:
+        assert np.array_equal(mi[0], ref_map), key
+        assert abs(int(tf[0]) - int(sparc_golden[key + "_t_final"])) <= 2, key
+    k = 4
+    np.testing.assert_allclose(nmse[0][:k], ref_nmse[:k], rtol=0, atol=1e-3, err_msg=key)
+
+
+def test_batched_decode_equals_single():
+    """A batch of codewords sharing one design decodes exactly like one-by-one."""
+    cp = {'P': 15.0, 'R': 1.3, 'L': 64, 'M': 64}
+    sparc.check_code_params(cp)
+    L, M = cp['L'], cp['M']
+    n = int(round(L * 6 / 1.3))
+    W = np.array(15.0)
+    o0, o1 = sparc.generate_ordering(W, n, L * M, 5)
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    rng = np.random.default_rng(0)
+    true = rng.integers(0, M, (9, L))
+    beta0 = np.zeros((9, L * M))
+    beta0[np.arange(9)[:, None], np.arange(L) * M + true] = 1
+    Y = op.apply(beta0, False) + rng.standard_normal((9, n))
+    for prec in (_native.SG_F64, _native.SG_F32):
+        mb, tb, nb, pb = sparc.amp_decode_batch(Y, op, 1.0, 25, true_idx=true, precision=prec)
+        for b in (0, 4, 8):
+            m1, t1, n1, p1 = sparc.amp_decode_batch(Y[b:b + 1], op, 1.0, 25, true_idx=true[b:b + 1],
+                                                    precision=prec)
+            assert np.array_equal(m1[0], mb[b]) and t1[0] == tb[b]
+            assert np.array_equal(n1[0], nb[b])
+
+
+def test_standalone_estimators():
+    rng = np.random.default_rng(3)
+    s = rng.standard_normal(64 * 32) * 5
+    tau = 0.7
+    np.testing.assert_allclose(sparc.msg_vector_mmse_estimator(s, tau, 32),
+                               sparc_ref.mmse_estimator(s, tau, 32), rtol=1e-12, atol=1e-300)
+    assert np.array_equal(sparc.msg_vector_map_estimator(s, 32), sparc_ref.map_estimator(s, 32))
+
+
+def _c2_design(seed, R=1.5):
+    L, M = 1024, 512
+    n = int(round(L * 9 / R))
+    W = np.array(15.0)
+    o0, o1 = sparc.generate_ordering(W, n, L * M, seed)
+    return W, L, M, n, o0, o1
+
+
+def test_full_size_operators():
+    W, L, M, n, o0, o1 = _c2_design(11)
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    assert op.w == 2 ** 20
+    Ab, Az = sparc_ref.dct_operators(W, L, M, n, o0, o1)
+    rng = np.random.default_rng(2)
+    x = rng.standard_normal(L * M)
+    y = rng.standard_normal(n)
+    assert _rel(op.Ab(x), Ab(x)) < 1e-12
+    assert _rel(op.Az(y), Az(y)) < 1e-12
+    assert _rel(op.apply(x, False, _native.SG_F32), Ab(x)) < 5e-6
+    assert _rel(op.apply(y, True, _native.SG_F32), Az(y)) < 5e-6
+
+
+def test_full_size_decode_r13_f32_and_f64():
+    """C2 geometry at R=1.3 (a decodable rate): every codeword of a batch
+    decodes with zero section errors in both precisions, and the f32 NMSE
+    trajectory tracks the f64 one."""
+    W, L, M, n, o0, o1 = _c2_design(21, R=1.3)
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    rng = np.random.default_rng(8)
+    B = 4
+    true = rng.integers(0, M, (B, L))
+    beta0 = np.zeros((B, L * M))
+    beta0[np.arange(B)[:, None], np.arange(L) * M + true] = 1
+    Y = op.apply(beta0, False) + rng.standard_normal((B, n))
+    m64, t64, n64, _ = sparc.amp_decode_batch(Y, op, 1.0, 25, true_idx=true)
+    m32, t32, n32, _ = sparc.amp_decode_batch(Y, op, 1.0, 25, true_idx=true, precision=_native.SG_F32)
+    assert np.array_equal(m64, true)
+    assert np.array_equal(m32, true)
+    assert np.all(np.abs(t64 - t32) <= 2)
+    np.testing.assert_allclose(n32[:, :8], n64[:, :8], atol=2e-3)
+
+
+def test_full_size_decode_f64_vs_oracle():
+    """One C2 codeword (R=1.5, the benchmark point) against the CPU restatement
+    (float128 softmax): identical t_final and MAP decisions, NMSE within 1e-8."""
+    W, L, M, n, o0, o1 = _c2_design(31)
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    Ab, Az = sparc_ref.dct_operators(W, L, M, n, o0, o1)
+    rng = np.random.RandomState(4)
+    true = rng.randint(0, M, L)
+    beta0 = np.zeros(L * M)
+    beta0[np.arange(L) * M + true] = 1
+    y = Ab(beta0) + rng.randn(n)
+    rb, rt, rn, rp = sparc_ref.amp(y, W, L, M, n, 1.0, 25, Ab, Az, beta0)
+    mi, tf, nm, ps = sparc.amp_decode_batch(y[None], op, 1.0, 25, true_idx=true[None])
+    assert tf[0] == rt
+    np.testing.assert_allclose(nm[0, :, 0], rn, atol=1e-8)
+    assert np.mean(mi[0] != np.argmax(rb.reshape(L, M), 1)) < 0.01
