@@ -1,0 +1,322 @@
+"""Benchmark of the AMP/BP decoding engine on MI355X.
+
+Headline (BASELINE.json metric, configs[1] = SURVEY.md 8(d) C2): batched SPARC
+AMP decoding, L=1024, M=512, regular design with the sub-sampled DCT operator
+(w = 2^20), R=1.5 (n=6144), P=15, sigma^2=1, t_max=25, 256 codewords per GPU
+per step.  One step = one AMP decode (reference sparc.py:883-999) of the
+batch, MAP decision and device-side error counting, plus -- with more than one
+GPU -- the RCCL all-reduce of the error counters.  Inputs are synthetic
+(random messages encoded with the same design, AWGN) and resident in HBM
+before the timed region.
+
+Secondary (C3): batched min-sum BP on 802.11n r1/2 z=81 (n=1944), 50
+iterations, 4096 codewords, reported in the "bp" object.
+
+Roofline: the AMP kernels of one iteration against HBM with SURVEY.md 8(d)'s
+algorithmic bytes per codeword-iteration 4*(2LM+4n); the BP kernel with
+4*(4*Nmsg+N) bytes per codeword-iteration.  Kernel durations come from HIP
+events recorded on the library stream around every launch in the timed region.
+
+CPU baseline: the CPU restatement in oracle/ (test infrastructure; here only as
+the timed baseline) on one host core, on a bounded sample (rank 0, N=1 only).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N>1: launched by torch.distributed.run, one process per GPU).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from ldpc_sparc_amd import _native, sparc  # noqa: E402
+from ldpc_sparc_amd.ldpc import code  # noqa: E402
+
+METRIC = "codewords/sec (AMP+BP) at L=1024 M=512 / n=1944; BER match vs CPU ref"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+AMP_PHASES = ("ab_passA", "ab_passB", "az_passA", "az_passB", "eta", "control")
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--rate", type=float, default=1.5)
+    ap.add_argument("--t-max", type=int, default=25)
+    ap.add_argument("--bp-batch", type=int, default=4096)
+    ap.add_argument("--bp-ebn0", type=float, default=2.0)
+    ap.add_argument("--bp-steps", type=int, default=10)
+    ap.add_argument("--no-bp", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="approximate CPU-baseline sample length (0 disables)")
+    ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
+    return ap.parse_args()
+
+
+class Dist:
+    """torch.distributed (gloo, CPU only) for rendezvous, barriers and the
+    RCCL unique id; all GPU work goes through libldpc_sparc_amd."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            self.dist = dist
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max(self, x):
+        if self.world == 1:
+            return x
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def bcast_bytes(self, b):
+        if self.world == 1:
+            return b
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
+
+    def close(self):
+        if self.world > 1:
+            self.dist.destroy_process_group()
+
+
+# ------------------------------------------------------------------ AMP (C2)
+
+def amp_setup(args, rank):
+    L, M = 1024, 512
+    logM = 9
+    n = int(round(L * logM / args.rate))
+    W = np.array(15.0)
+    prec = _native.SG_F32 if args.precision == "f32" else _native.SG_F64
+    o0, o1 = sparc.generate_ordering(W, n, L * M, 0)  # one design shared by every rank
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    plan = op.plan(prec)
+    B = args.batch
+    rng = np.random.default_rng(1000 + rank)
+    true = rng.integers(0, M, (B, L)).astype(np.int32)
+    # encode x = A beta0 on the GPU (sparc.py:51), add AWGN (sparc_sim.py:179-204)
+    beta0 = np.zeros((B, L * M))
+    beta0[np.arange(B)[:, None], np.arange(L) * M + true] = 1.0
+    X = op.apply(beta0, False, _native.SG_F64)
+    del beta0
+    Y = X + rng.standard_normal((B, n))
+    dt = np.float32 if prec == _native.SG_F32 else np.float64
+    st = dict(L=L, M=M, logM=logM, n=n, B=B, op=op, plan=plan, prec=prec,
+              d_y=_native.DeviceBuffer.from_array(Y.astype(dt)),
+              d_true=_native.DeviceBuffer.from_array(true),
+              d_map=_native.DeviceBuffer(B * L * 4), d_tf=_native.DeviceBuffer(B * 4),
+              d_cnt=_native.DeviceBuffer(4 * 8), W=W, o0=o0, o1=o1, Y=Y, true=true)
+    return st
+
+
+def amp_step(st, args, comm):
+    lib = _native.lib()
+    _native.check(lib.sg_memset(st["d_cnt"].ptr, 0, 32, None))
+    _native.check(lib.sg_amp_decode_device(st["plan"], st["d_y"].ptr, st["B"], st["d_true"].ptr, 1.0,
+                                           args.t_max, 1e-6, 1, st["d_map"].ptr, st["d_tf"].ptr,
+                                           None, None, None))
+    _native.check(lib.sg_amp_count_errors_device(st["d_map"].ptr, st["d_true"].ptr, st["d_tf"].ptr,
+                                                 st["B"], st["L"], st["logM"], st["d_cnt"].ptr, None))
+    if comm is not None:
+        comm.allreduce_sum_i64(st["d_cnt"], 4)
+
+
+def amp_cpu_baseline(st, args, seconds):
+    """oracle/sparc_ref.py (scipy DCT operators, float128 softmax as the
+    reference) on one core, on as many codewords of the same batch as fit."""
+    from oracle import sparc_ref
+    L, M, n = st["L"], st["M"], st["n"]
+    Ab, Az = sparc_ref.dct_operators(st["W"], L, M, n, st["o0"], st["o1"])
+    t0 = time.perf_counter()
+    done = iters = 0
+    while True:
+        b = done
+        beta0 = np.zeros(L * M)
+        beta0[np.arange(L) * M + st["true"][b]] = 1.0
+        _, tf, _, _ = sparc_ref.amp(st["Y"][b], st["W"], L, M, n, 1.0, args.t_max, Ab, Az, beta0)
+        done += 1
+        iters += tf
+        el = time.perf_counter() - t0
+        if el >= seconds or done >= st["B"]:
+            break
+    return {"value": done / el, "unit": "codewords/s", "cores": 1, "kind": "port",
+            "sample": f"{done} C2 codewords (R={args.rate}, t_max={args.t_max}, {iters} AMP "
+                      f"iterations, {el:.1f} s) decoded by oracle/sparc_ref.py (numpy/scipy "
+                      f"fftpack DCT, float128 softmax) on 1 host core"}
+
+
+# ------------------------------------------------------------------ BP (C3)
+
+def bp_setup(args, rank):
+    c = code("802.11n", "1/2", 81)
+    B = args.bp_batch
+    rng = np.random.default_rng(2000 + rank)
+    X = c.encode_batch(rng.integers(0, 2, (B, c.K)))
+    R = c.K / c.N
+    s2 = 1 / (2 * R * 10 ** (args.bp_ebn0 / 10))
+    ch = 2 * ((1 - 2 * X) + np.sqrt(s2) * rng.standard_normal(X.shape)) / s2
+    g = c._device_graph()
+    return dict(c=c, B=B, g=g, ch=ch, X=X,
+                d_ch=_native.DeviceBuffer.from_array(ch.astype(np.float32)),
+                d_app=_native.DeviceBuffer(B * c.N * 4), d_it=_native.DeviceBuffer(B * 4),
+                d_x=_native.DeviceBuffer.from_array(X.astype(np.uint8)),
+                d_cnt=_native.DeviceBuffer(32))
+
+
+def bp_step(st):
+    lib = _native.lib()
+    c = st["c"]
+    _native.check(lib.sg_memset(st["d_cnt"].ptr, 0, 32, None))
+    _native.check(lib.sg_ldpc_decode_device(st["g"], _native.SG_MINSUM, _native.SG_F32, st["d_ch"].ptr,
+                                            st["B"], 50, 0.7, st["d_app"].ptr, st["d_it"].ptr, None))
+    _native.check(lib.sg_ldpc_count_errors_device(st["g"], _native.SG_F32, st["d_app"].ptr, st["d_x"].ptr,
+                                                  st["d_it"].ptr, st["B"], c.K, st["d_cnt"].ptr, None))
+
+
+def bp_cpu_baseline(st, seconds):
+    """oracle/bp_oracle.c min-sum (reference c_ldpc.c with the loop index
+    corrected) on one host core."""
+    from oracle import bp
+    c = st["c"]
+    t0 = time.perf_counter()
+    done = 0
+    while True:
+        chunk = st["ch"][done:done + 64]
+        bp.decode_batch("minsum", chunk, c.vdeg, c.cdeg, c.intrlv, 50, 0.7)
+        done += len(chunk)
+        el = time.perf_counter() - t0
+        if el >= seconds or done >= st["B"]:
+            break
+    return {"value": done / el, "unit": "codewords/s", "cores": 1, "kind": "port",
+            "sample": f"{done} C3 codewords (802.11n r1/2 z=81, min-sum, 50 it, Eb/N0 "
+                      f"{st.get('ebn0')} dB) by oracle/bp_oracle.c on 1 host core"}
+
+
+def main():
+    args = parse()
+    d = Dist()
+    _native.require_gpu()
+    ndev = _native.device_count()
+    _native.check(_native.lib().sg_set_device(d.local % max(ndev, 1)))
+    comm = None
+    if d.world > 1:
+        uid = d.bcast_bytes(_native.Comm.unique_id() if d.rank == 0 else None)
+        comm = _native.Comm(d.world, d.rank, uid)
+
+    st = amp_setup(args, d.rank)
+    for _ in range(args.warmup):
+        amp_step(st, args, comm)
+    _native.device_synchronize()
+    prof = _native.Profiler()
+    d.barrier()
+    _native.device_synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        amp_step(st, args, comm)
+    _native.device_synchronize()
+    el = time.perf_counter() - t0
+    phases = prof.stop()
+    el_max = d.max(el)
+    cnt = st["d_cnt"].download(np.zeros(4, np.int64))  # last step, summed over ranks
+    tf = st["d_tf"].download(np.zeros(st["B"], np.int32))
+    cw_it = int(tf.sum()) * args.steps  # executed codeword-iterations on this rank
+    amp_ms = sum(phases.get(p, (0.0, 0))[0] for p in AMP_PHASES)
+    bytes_per_cwit = 4 * (2 * st["L"] * st["M"] + 4 * st["n"])
+    achieved = bytes_per_cwit * cw_it / (amp_ms * 1e-3) / 1e9 if amp_ms > 0 else None
+    total_cw = d.world * st["B"] * args.steps
+    out = {
+        "metric": METRIC,
+        "value": total_cw / el_max,
+        "unit": "codewords/s",
+        "n_gpus": d.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * el_max / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32" if st["prec"] == _native.SG_F32 else "f64",
+        "data": "synthetic: random messages, encoded x = A beta0 with the benchmark design, AWGN "
+                "sigma^2=1 (host numpy RNG), resident in HBM before timing",
+        "config": {"workload": "C2: SPARC AMP, regular design, sub-sampled DCT operator w=2^20",
+                   "L": st["L"], "M": st["M"], "n": st["n"], "R": args.rate, "P": 15.0,
+                   "awgn_var": 1.0, "t_max": args.t_max, "batch_per_gpu": st["B"],
+                   "parallelism": f"mc-shard x{d.world} (independent codewords per GPU, "
+                                  "RCCL all-reduce of error counters)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                     "kernel": "one AMP iteration = " + "+".join(AMP_PHASES),
+                     "algorithmic_bytes_per_codeword_iteration": bytes_per_cwit,
+                     "codeword_iterations": cw_it,
+                     "kernel_ms": {k: round(v[0], 3) for k, v in phases.items()},
+                     "launches": {k: v[1] for k, v in phases.items()}},
+        "amp": {"avg_iterations": float(tf.mean()), "section_errors": int(cnt[0]),
+                "bit_errors": int(cnt[1]), "codeword_errors": int(cnt[2]),
+                "ber": float(cnt[1]) / (d.world * st["B"] * st["L"] * st["logM"])},
+    }
+
+    if not args.no_bp:
+        bst = bp_setup(args, d.rank)
+        bst["ebn0"] = args.bp_ebn0
+        for _ in range(2):
+            bp_step(bst)
+        _native.device_synchronize()
+        prof = _native.Profiler()
+        d.barrier()
+        _native.device_synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.bp_steps):
+            bp_step(bst)
+        _native.device_synchronize()
+        bel = d.max(time.perf_counter() - t0)
+        ph = prof.stop()
+        its = bst["d_it"].download(np.zeros(bst["B"], np.int32))
+        bcnt = bst["d_cnt"].download(np.zeros(4, np.int64))
+        c = bst["c"]
+        exec_it = np.where(its < 50, its + 1, 50)  # executed iterations per codeword
+        bp_ms = ph.get("bp_flood", (0.0, 0))[0]
+        bbytes = 4 * (4 * c.Nmsg + c.N)
+        bach = bbytes * exec_it.sum() * args.bp_steps / (bp_ms * 1e-3) / 1e9 if bp_ms else None
+        out["bp"] = {"workload": "C3: 802.11n r1/2 z=81 (n=1944), min-sum (corr 0.7), max 50 it, "
+                                 f"Eb/N0 {args.bp_ebn0} dB, random codewords",
+                     "value": d.world * bst["B"] * args.bp_steps / bel, "unit": "codewords/s",
+                     "batch_per_gpu": bst["B"], "avg_executed_iterations": float(exec_it.mean()),
+                     "frame_errors": int(bcnt[1]), "bit_errors": int(bcnt[0]),
+                     "roofline": {"bound": "hbm", "achieved": bach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": bach / HBM_PEAK_GBS if bach else None, "traffic": None,
+                                  "kernel": "bp_flood_kernel<float, minsum>",
+                                  "algorithmic_bytes_per_codeword_iteration": bbytes,
+                                  "kernel_ms": bp_ms, "launches": ph.get("bp_flood", (0, 0))[1]}}
+
+    if d.rank == 0 and d.world == 1 and args.cpu_seconds > 0:
+        out["cpu_baseline"] = amp_cpu_baseline(st, args, args.cpu_seconds)
+        if not args.no_bp:
+            out["bp"]["cpu_baseline"] = bp_cpu_baseline(bst, args.cpu_seconds / 3)
+    if d.rank == 0:
+        print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.destroy()
+    d.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -60,6 +60,30 @@ int sg_event_create(void **ev);
 int sg_event_destroy(void *ev);
 int sg_event_record(void *ev, void *stream);
 int sg_event_elapsed_ms(void *start, void *stop, float *ms);
+int sg_device_synchronize(void);
+
+/* Per-phase kernel timing.  When enabled, every kernel launch of the decoders
+ * is bracketed by HIP events on the stream it is launched on; collect
+ * synchronises the pending events, returns the summed milliseconds and the
+ * launch count per phase (arrays of SG_PH_COUNT) and resets the counters. */
+enum sg_phase {
+    SG_PH_AB_A = 0, SG_PH_AB_B = 1, SG_PH_AZ_A = 2, SG_PH_AZ_B = 3, SG_PH_ETA = 4,
+    SG_PH_CONTROL = 5, SG_PH_BP = 6, SG_PH_DENSE = 7, SG_PH_COUNT = 8
+};
+int sg_profile_enable(int on);
+int sg_profile_collect(double *total_ms, int64_t *launches);
+const char *sg_phase_name(int phase);
+
+/* ------------------------------------------------------------- multi-GPU */
+/* One RCCL communicator per process (one process per GPU).  Rank 0 creates
+ * the 128-byte unique id, the launcher distributes it, every rank calls init.
+ * New capability: the reference parallelises only by independent processes
+ * (ldpc_jossy/py/ldpc_awgn.py:125-131). */
+typedef struct sg_comm sg_comm;
+int sg_comm_unique_id(void *id_out /* 128 bytes */);
+int sg_comm_init(int nranks, int rank, const void *id, sg_comm **out);
+int sg_comm_allreduce_sum_i64(sg_comm *c, int64_t *d_buf, size_t count, void *stream);
+int sg_comm_destroy(sg_comm *c);
 
 /* ------------------------------------------------------------------- LDPC */
 typedef struct sg_graph sg_graph;

@@ -76,7 +76,17 @@ SIGNATURES = [
     ("sg_section_softmax", ct.c_int, [vp, ct.c_int, ct.c_int, ct.c_double, vp]),
     ("sg_section_argmax", ct.c_int, [vp, ct.c_int, ct.c_int, vp]),
     ("Lxfb", ct.c_double, [dp, ct.c_long, ct.c_int]),
+    ("sg_device_synchronize", ct.c_int, []),
+    ("sg_profile_enable", ct.c_int, [ct.c_int]),
+    ("sg_profile_collect", ct.c_int, [vp, vp]),
+    ("sg_phase_name", ct.c_char_p, [ct.c_int]),
+    ("sg_comm_unique_id", ct.c_int, [vp]),
+    ("sg_comm_init", ct.c_int, [ct.c_int, ct.c_int, vp, ct.POINTER(vp)]),
+    ("sg_comm_allreduce_sum_i64", ct.c_int, [vp, vp, ct.c_size_t, vp]),
+    ("sg_comm_destroy", ct.c_int, [vp]),
 ]
+
+SG_PH_COUNT = 8
 
 
 def lib():
@@ -187,3 +197,54 @@ class Event:
             lib().sg_event_destroy(self.ev)
         except Exception:
             pass
+
+
+def device_synchronize():
+    check(lib().sg_device_synchronize())
+
+
+class Profiler:
+    """Per-phase kernel timing through HIP events on the launch streams
+    (sg_profile_enable / sg_profile_collect)."""
+
+    def __init__(self):
+        check(lib().sg_profile_enable(1))
+        self.collect()  # drop anything recorded before
+
+    def collect(self):
+        ms = np.zeros(SG_PH_COUNT)
+        n = np.zeros(SG_PH_COUNT, dtype=np.int64)
+        check(lib().sg_profile_collect(ptr(ms), ptr(n)))
+        return {lib().sg_phase_name(i).decode(): (float(ms[i]), int(n[i]))
+                for i in range(SG_PH_COUNT) if n[i]}
+
+    def stop(self):
+        check(lib().sg_profile_enable(0))
+        return self.collect()
+
+
+class Comm:
+    """RCCL communicator of this process (one process per GPU)."""
+
+    ID_BYTES = 128
+
+    @staticmethod
+    def unique_id():
+        buf = (ct.c_char * Comm.ID_BYTES)()
+        check(lib().sg_comm_unique_id(ct.cast(buf, ct.c_void_p)))
+        return bytes(buf)
+
+    def __init__(self, nranks, rank, uid):
+        assert len(uid) == Comm.ID_BYTES
+        self._id = (ct.c_char * Comm.ID_BYTES).from_buffer_copy(uid)
+        h = ct.c_void_p()
+        check(lib().sg_comm_init(int(nranks), int(rank), ct.cast(self._id, ct.c_void_p), ct.byref(h)))
+        self.h = h
+
+    def allreduce_sum_i64(self, dbuf, count, stream=None):
+        check(lib().sg_comm_allreduce_sum_i64(self.h, dbuf.ptr, int(count), stream))
+
+    def destroy(self):
+        if self.h is not None:
+            lib().sg_comm_destroy(self.h)
+            self.h = None

@@ -521,10 +521,16 @@ int amp_launch_ab(const AmpTables<T> &tb, const AmpBufs<T> &bf, hipStream_t s) {
     SG_TRY(set_lds_limits<T>());
     int CT, nthr, ept;
     col_geometry(tb.P, tb.Q, sizeof(T) == 8, &CT, &nthr, &ept);
-    SG_EPT_DISPATCH(ept, launch_abA, T, tb, bf, CT, nthr, s);
+    {
+        ProfScope ps(SG_PH_AB_A, s);
+        SG_EPT_DISPATCH(ept, launch_abA, T, tb, bf, CT, nthr, s);
+    }
     SG_HIP(hipGetLastError());
     row_geometry(tb.Q, &nthr, &ept);
-    SG_EPT_DISPATCH(ept, launch_abB, T, tb, bf, nthr, s);
+    {
+        ProfScope ps(SG_PH_AB_B, s);
+        SG_EPT_DISPATCH(ept, launch_abB, T, tb, bf, nthr, s);
+    }
     SG_HIP(hipGetLastError());
     return SG_OK;
 }
@@ -535,10 +541,16 @@ int amp_launch_az(const AmpTables<T> &tb, const AmpBufs<T> &bf, hipStream_t s) {
     SG_TRY(set_lds_limits<T>());
     int CT, nthr, ept;
     row_geometry(tb.Q, &nthr, &ept);
-    SG_EPT_DISPATCH(ept, launch_azA, T, tb, bf, nthr, s);
+    {
+        ProfScope ps(SG_PH_AZ_A, s);
+        SG_EPT_DISPATCH(ept, launch_azA, T, tb, bf, nthr, s);
+    }
     SG_HIP(hipGetLastError());
     col_geometry(tb.P, tb.Q, sizeof(T) == 8, &CT, &nthr, &ept);
-    SG_EPT_DISPATCH(ept, launch_azB, T, tb, bf, CT, nthr, s);
+    {
+        ProfScope ps(SG_PH_AZ_B, s);
+        SG_EPT_DISPATCH(ept, launch_azB, T, tb, bf, CT, nthr, s);
+    }
     SG_HIP(hipGetLastError());
     return SG_OK;
 }
@@ -549,6 +561,7 @@ int amp_launch_eta(const AmpTables<T> &tb, const AmpBufs<T> &bf, hipStream_t s) 
     const int waves = 4;
     dim3 grid((tb.L + waves - 1) / waves, bf.B);
     const int epl = (tb.M + 63) / 64;
+    ProfScope ps(SG_PH_ETA, s);
     if (epl <= 1) hipLaunchKernelGGL((eta_kernel<T, 1>), grid, dim3(64 * waves), 0, s, tb, bf);
     else if (epl <= 2) hipLaunchKernelGGL((eta_kernel<T, 2>), grid, dim3(64 * waves), 0, s, tb, bf);
     else if (epl <= 4) hipLaunchKernelGGL((eta_kernel<T, 4>), grid, dim3(64 * waves), 0, s, tb, bf);
@@ -564,6 +577,7 @@ template <typename T>
 int amp_launch_control(const AmpTables<T> &tb, const AmpBufs<T> &bf, const AmpScalars &sc, const AmpParams &pr,
                        int phase, int t, hipStream_t s) {
     if (bf.B <= 0) return SG_OK;
+    ProfScope ps(SG_PH_CONTROL, s);
     hipLaunchKernelGGL((control_kernel<T>), dim3(bf.B), dim3(256), 0, s, tb, bf, sc, pr, phase, t);
     SG_HIP(hipGetLastError());
     return SG_OK;

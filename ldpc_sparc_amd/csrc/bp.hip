@@ -179,6 +179,7 @@ static int launch_one(const BpArgs<T> &a, size_t lds, hipStream_t s) {
     if (grid > a.B) grid = a.B;
     if (lds > 64 * 1024)
         SG_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    ProfScope ps(SG_PH_BP, s);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(BP_THREADS), lds, s, a);
     SG_HIP(hipGetLastError());
     return SG_OK;

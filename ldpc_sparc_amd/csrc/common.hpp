@@ -21,6 +21,17 @@ hipStream_t lib_stream();
 inline hipStream_t pick_stream(void *s) { return s ? reinterpret_cast<hipStream_t>(s) : lib_stream(); }
 int device_cu_count();
 
+// Per-phase device timing (sg_profile_enable): HIP events recorded on the
+// stream a phase is launched on, resolved by sg_profile_collect.
+int prof_begin(int phase, hipStream_t s);
+void prof_end(int token, hipStream_t s);
+struct ProfScope {
+    int tok;
+    hipStream_t s;
+    ProfScope(int phase, hipStream_t st) : tok(prof_begin(phase, st)), s(st) {}
+    ~ProfScope() { prof_end(tok, s); }
+};
+
 struct HipError {
     hipError_t err;
     const char *what;

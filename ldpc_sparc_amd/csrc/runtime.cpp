@@ -80,6 +80,44 @@ int device_cu_count() {
     return g_cus[d];
 }
 
+// ---------------------------------------------------------------- profiling
+struct ProfRec {
+    int phase;
+    hipEvent_t a, b;
+};
+static bool g_prof_on = false;
+static std::vector<ProfRec> g_prof_pending;
+static std::vector<hipEvent_t> g_ev_pool;
+static double g_prof_ms[SG_PH_COUNT] = {0};
+static int64_t g_prof_n[SG_PH_COUNT] = {0};
+
+static hipEvent_t ev_get() {
+    if (!g_ev_pool.empty()) {
+        hipEvent_t e = g_ev_pool.back();
+        g_ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+int prof_begin(int phase, hipStream_t s) {
+    if (!g_prof_on) return -1;
+    std::lock_guard<std::mutex> lk(g_mu);
+    ProfRec r{phase, ev_get(), ev_get()};
+    if (!r.a || !r.b) return -1;
+    hipEventRecord(r.a, s);
+    g_prof_pending.push_back(r);
+    return (int)g_prof_pending.size() - 1;
+}
+
+void prof_end(int tok, hipStream_t s) {
+    if (tok < 0) return;
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (tok < (int)g_prof_pending.size()) hipEventRecord(g_prof_pending[tok].b, s);
+}
+
 }  // namespace sg
 
 using namespace sg;
@@ -150,6 +188,46 @@ int sg_memset(void *dptr, int value, size_t bytes, void *stream) {
 int sg_stream_synchronize(void *stream) {
     SG_TRY(ensure_device());
     SG_HIP(hipStreamSynchronize(pick_stream(stream)));
+    return SG_OK;
+}
+
+int sg_profile_enable(int on) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_prof_on = on != 0;
+    return SG_OK;
+}
+
+int sg_profile_collect(double *total_ms, int64_t *launches) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (auto &r : g_prof_pending) {
+        float ms = 0.f;
+        if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess &&
+            r.phase >= 0 && r.phase < SG_PH_COUNT) {
+            g_prof_ms[r.phase] += ms;
+            g_prof_n[r.phase] += 1;
+        }
+        g_ev_pool.push_back(r.a);
+        g_ev_pool.push_back(r.b);
+    }
+    g_prof_pending.clear();
+    for (int i = 0; i < SG_PH_COUNT; ++i) {
+        if (total_ms) total_ms[i] = g_prof_ms[i];
+        if (launches) launches[i] = g_prof_n[i];
+        g_prof_ms[i] = 0.0;
+        g_prof_n[i] = 0;
+    }
+    return SG_OK;
+}
+
+const char *sg_phase_name(int phase) {
+    static const char *names[SG_PH_COUNT] = {"ab_passA", "ab_passB", "az_passA", "az_passB", "eta",
+                                             "control", "bp_flood", "dense_gemm"};
+    return (phase >= 0 && phase < SG_PH_COUNT) ? names[phase] : "unknown";
+}
+
+int sg_device_synchronize(void) {
+    SG_TRY(ensure_device());
+    SG_HIP(hipDeviceSynchronize());
     return SG_OK;
 }
 
