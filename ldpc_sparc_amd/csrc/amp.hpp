@@ -62,6 +62,81 @@ struct AmpParams {
     int phi_method, t_max;
 };
 
+// ------------------------------------------------------------------------
+// Regular engine (amp_fused.hip): designs with one transform per column block
+// (W.ndim 0 or 1, every W entry nonzero).  See DESIGN.md "AMP engine".
+//
+// Complex w-space index m = Q*m1 + m2.  A "class" is the residue m2: the P
+// complex slots {Q*m1 + m2}.  The decoder keeps s (sparc.py:972) per codeword
+// in CLASS ORDER: entries of a column block sorted by (class, section, j), so
+// the P-point FFT stage of each class reads and writes its slice of s
+// contiguously and the reference's random orders (generate_ordering,
+// sparc.py:735-775) become LDS scatters.  Only the rows k1 that hold needed
+// outputs of the forward transform (= nonzero inputs of the inverse) cross
+// HBM between the two FFT stages ("needed rows", compact index rho).
+template <typename T>
+struct RegTables {
+    int nT, L, M, LM, n, Lc, Mc, Lblk;  // Lblk = sections per column block
+    int N2, P, Q, log2P;
+    int nRmax, nKmax, RB, nrb;          // needed rows / indices (max over t), row-block size, #row blocks
+    int maxKb;                          // most needed indices in one row block
+    const int32_t *nR;       // [nT]
+    const int32_t *row_k1;   // [nT][nRmax]
+    const int32_t *kptr;     // [nT][nRmax+1] needed indices of each row (CSR, within t)
+    const int32_t *kk2;      // [nT][nKmax]
+    const int32_t *krho;     // [nT][nKmax]
+    const int32_t *oa, *ob;  // [nT][n] forward outputs: X = Re(c1 X[oa] + c2 conj X[ob])
+    const cx<T> *oc;         // [nT][n][2]
+    const int32_t *gi;       // [nT][nKmax][4] inverse inputs: G[k] = sum c * z[i]/phi
+    const cx<T> *gc;         // [nT][nKmax][4]
+    const int32_t *cls_ptr;  // [nT][Q+1]
+    const uint16_t *cls_loc; // [nT][Mc] real LDS index 2*m1 + component
+    const uint16_t *cls_sec; // [nT][Mc] section within the block
+    const int32_t *cls_j;    // [nT][Mc] column index within the block
+    const int32_t *qpos;     // [nT][Mc] column index -> class-order position
+    const uint16_t *seg;     // [nT][Q][Lblk+1] section segments within a class
+    const cx<T> *twP, *twQ, *twHi, *twLo;
+    const cx<T> *stw;         // per-stage P-point FFT twiddles (lds_fft1)
+    const cx<T> *twa, *twb;   // w_N2^(m2 k1) = twa[m2][k1 & 63] * twb[m2][k1 >> 6]
+    int nB;                   // ceil(P / 64)
+};
+
+template <typename T>
+struct RegBufs {
+    int B;
+    int mode;               // 0: decode; 1: operator application (ext_in / ext_out)
+    T *s;                   // [B][LM] class order
+    cx<T> *tu;              // [B][nT][Q][nRmax]
+    cx<T> *xn;              // [B][nT][nKmax]
+    T *part;                // [B][nT][Q][3][Lblk] per-class section max, sum e, sum e^2
+    T *stM, *stI;           // [B][L] section max of s, 1/sum
+    const T *y;             // [B][n]
+    T *z;                   // [B][n]
+    double *phi, *tau, *tau_prev;  // [B], [B][Lc], [B][Lc]
+    int32_t *active;        // [B]
+    const int32_t *true_idx;  // [B][L] or null
+    int32_t *map;           // [B][L]
+    const T *ext_in;        // mode 1: [B][LM] (Ab) or [B][n] (Az)
+    T *ext_out;             // mode 1: [B][n] (Ab) or [B][LM] (Az)
+};
+
+template <typename T>
+int reg_launch_ab(const RegTables<T> &tb, const RegBufs<T> &bf, hipStream_t s);
+template <typename T>
+int reg_launch_az(const RegTables<T> &tb, const RegBufs<T> &bf, int t_iter, hipStream_t s);
+template <typename T>
+int reg_launch_ctrl0(const RegTables<T> &tb, const RegBufs<T> &bf, const AmpScalars &sc, const AmpParams &pr,
+                     int t, hipStream_t s);
+template <typename T>
+int reg_launch_merge(const RegTables<T> &tb, const RegBufs<T> &bf, const AmpScalars &sc, const AmpParams &pr,
+                     int t, hipStream_t s);
+template <typename T>
+int reg_launch_map(const RegTables<T> &tb, const RegBufs<T> &bf, hipStream_t s);
+template <typename T>
+int reg_launch_ab_finish(const RegTables<T> &tb, const RegBufs<T> &bf, hipStream_t s);
+size_t reg_stage1_lds(int P, int Lblk, size_t real_bytes);
+int reg_launch_init(int B, int Lc, int t_max, double *nmse, int32_t *active, int32_t *t_final, hipStream_t s);
+
 template <typename T>
 int amp_launch_ab(const AmpTables<T> &tb, const AmpBufs<T> &bf, hipStream_t s);   // beta -> rbuf
 template <typename T>

@@ -1,0 +1,660 @@
+// Regular-design AMP engine on gfx950: SPARCs whose base matrix has one
+// transform per column block (W.ndim 0 or 1 -- the regular design of the
+// benchmark, sparc.py:777-849, and power allocation).
+//
+// Reference: sparc_public/sparc.py sparc_amp :883-999, sub_dct :648-701,
+// msg_vector_mmse_estimator :402-465, msg_vector_map_estimator :467-512.
+//
+// One AMP iteration (DESIGN.md "AMP engine") is six launches:
+//   ab_stage1  (class m2)   beta = softmax(s) from (s, section max, 1/sum) in
+//                           class order -> LDS scatter -> P-point FFT ->
+//                           twiddle -> needed rows T[m2][rho]
+//   ab_stage2  (row block)  Q-point DFT of each needed row at the needed
+//                           frequencies -> X[k] (k in the needed set)
+//   ctrl0      (codeword)   z = y - Re(c1 X[a] + c2 conj X[b]) + b z,
+//                           phi, tau (sparc.py:931-969)
+//   az_stage1  (row block)  G[k] from z/phi (<= 4 terms), inverse Q-point
+//                           DFT of the sparse rows, conjugate twiddle -> U
+//   az_stage2  (class m2)   U rows -> LDS -> inverse P-point FFT -> u in
+//                           class order; s = beta + tau u (sparc.py:972);
+//                           per-(class, section) max / sum e / sum e^2
+//   merge      (codeword)   section max and 1/sum, sum beta^2 = S2/S1^2,
+//                           beta at the true index -> psi, NMSE, early stop
+//                           (sparc.py:973-988)
+// beta itself never reaches HBM: it is recomputed from s where needed.
+#include "amp.hpp"
+
+namespace sg {
+
+template <typename T>
+__device__ __forceinline__ T rexp(T x);
+template <>
+__device__ __forceinline__ float rexp<float>(float x) { return __expf(x); }
+template <>
+__device__ __forceinline__ double rexp<double>(double x) { return exp(x); }
+
+// Exponent argument (v - m) / tau of the section softmax.  Double precision
+// follows the reference's x = s / tau, x - max(x) (sparc.py:430-431); single
+// precision multiplies by 1/tau.
+template <typename T>
+__device__ __forceinline__ T sm_arg(T v, T m, T tau, T inv_tau);
+template <>
+__device__ __forceinline__ float sm_arg<float>(float v, float m, float, float inv_tau) { return (v - m) * inv_tau; }
+template <>
+__device__ __forceinline__ double sm_arg<double>(double v, double m, double tau, double) { return v / tau - m / tau; }
+
+// w_N2^(m2 k1), m2 < Q, k1 < P, from two small tables (contiguous per m2)
+template <typename T>
+__device__ __forceinline__ cx<T> reg_tw2(const RegTables<T> &tb, int m2, int k1) {
+    return cmul(tb.twa[m2 * 64 + (k1 & 63)], tb.twb[m2 * tb.nB + (k1 >> 6)]);
+}
+
+__device__ __forceinline__ double reg_block_sum(double v, double *red) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    double t = 0.0;
+    for (int w = 0; w < nw; ++w) t += red[w];
+    return t;
+}
+
+constexpr int REG_CH = 8;  // entries a thread loads before using them
+
+size_t reg_stage1_lds(int P, int Lblk, size_t real_bytes) {
+    return (size_t)P * 2 * real_bytes + (size_t)2 * Lblk * real_bytes;
+}
+
+// ------------------------------------------------------------------ ab stage 1
+template <typename T, int EPT>
+__global__ __launch_bounds__(1024) void reg_ab_stage1(RegTables<T> tb, RegBufs<T> bf) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cx<T> *d = reinterpret_cast<cx<T> *>(smem);
+    T *dr = reinterpret_cast<T *>(smem);
+    T *sM = dr + 2 * (size_t)tb.P;
+    T *sI = sM + tb.Lblk;
+    const int m2 = blockIdx.x, t = blockIdx.y, cw = blockIdx.z;
+    if (bf.mode == 0 && !bf.active[cw]) return;
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    for (int i = tid; i < 2 * tb.P; i += nthr) dr[i] = T(0);
+    const size_t tc = (size_t)t * tb.Mc;
+    T tau = T(1), inv_tau = T(1);
+    if (bf.mode == 0) {
+        const size_t lb = (size_t)cw * tb.L + (size_t)t * tb.Lblk;
+        for (int l = tid; l < tb.Lblk; l += nthr) {
+            sM[l] = bf.stM[lb + l];
+            sI[l] = bf.stI[lb + l];
+        }
+        const double tv = bf.tau[(size_t)cw * tb.Lc + t];
+        tau = (T)tv;
+        inv_tau = (T)(1.0 / tv);
+    }
+    __syncthreads();
+    const int32_t *cp = tb.cls_ptr + (size_t)t * (tb.Q + 1);
+    const int q0 = cp[m2], q1 = cp[m2 + 1];
+    const uint16_t *loc = tb.cls_loc + tc;
+    if (bf.mode == 0) {
+        const T *s = bf.s + (size_t)cw * tb.LM + tc;
+        const uint16_t *sec = tb.cls_sec + tc;
+        for (int base = q0 + tid; base < q1; base += REG_CH * nthr) {
+            T v[REG_CH];
+            int lc[REG_CH], sc[REG_CH];
+#pragma unroll
+            for (int i = 0; i < REG_CH; ++i) {  // issue every load of the chunk first
+                const int q = base + i * nthr;
+                if (q < q1) {
+                    v[i] = s[q];
+                    lc[i] = loc[q];
+                    sc[i] = sec[q];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < REG_CH; ++i)
+                if (base + i * nthr < q1)
+                    dr[lc[i]] = rexp<T>(sm_arg<T>(v[i], sM[sc[i]], tau, inv_tau)) * sI[sc[i]];
+        }
+    } else {
+        const T *x = bf.ext_in + (size_t)cw * tb.LM + tc;
+        const int32_t *cj = tb.cls_j + tc;
+        for (int q = q0 + tid; q < q1; q += nthr) dr[loc[q]] = x[cj[q]];
+    }
+    __syncthreads();
+    lds_fft1<T, false, EPT>(d, tb.log2P, tb.stw, tid, nthr);
+    const int nR = tb.nR[t];
+    const int32_t *rk = tb.row_k1 + (size_t)t * tb.nRmax;
+    cx<T> *out = bf.tu + (((size_t)cw * tb.nT + t) * tb.Q + m2) * tb.nRmax;
+    for (int base = tid; base < nR; base += REG_CH * nthr) {
+        int k1[REG_CH];
+        cx<T> w[REG_CH];
+#pragma unroll
+        for (int i = 0; i < REG_CH; ++i) {
+            const int r = base + i * nthr;
+            k1[i] = r < nR ? rk[r] : 0;
+        }
+#pragma unroll
+        for (int i = 0; i < REG_CH; ++i) w[i] = reg_tw2(tb, m2, k1[i]);
+#pragma unroll
+        for (int i = 0; i < REG_CH; ++i) {
+            const int r = base + i * nthr;
+            if (r < nR) out[r] = cmul(d[k1[i]], w[i]);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ ab stage 2
+template <typename T>
+__global__ __launch_bounds__(256) void reg_ab_stage2(RegTables<T> tb, RegBufs<T> bf) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cx<T> *d = reinterpret_cast<cx<T> *>(smem);  // [Q][RB]
+    cx<T> *twq = d + (size_t)tb.Q * tb.RB;       // [Q]
+    const int rb = blockIdx.x, t = blockIdx.y, cw = blockIdx.z;
+    if (bf.mode == 0 && !bf.active[cw]) return;
+    const int nR = tb.nR[t];
+    const int r0 = rb * tb.RB;
+    if (r0 >= nR) return;
+    const int r1 = min(nR, r0 + tb.RB), nr = r1 - r0;
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    for (int i = tid; i < tb.Q; i += nthr) twq[i] = tb.twQ[i];
+    const cx<T> *src = bf.tu + ((size_t)cw * tb.nT + t) * tb.Q * tb.nRmax;
+    for (int e = tid; e < tb.Q * nr; e += nthr) {
+        const int m2 = e / nr, r = e - m2 * nr;
+        d[m2 * tb.RB + r] = src[(size_t)m2 * tb.nRmax + r0 + r];
+    }
+    __syncthreads();
+    const int32_t *kp = tb.kptr + (size_t)t * (tb.nRmax + 1);
+    const int ka = kp[r0], kb = kp[r1];
+    const int32_t *kr = tb.krho + (size_t)t * tb.nKmax, *k2s = tb.kk2 + (size_t)t * tb.nKmax;
+    cx<T> *xn = bf.xn + ((size_t)cw * tb.nT + t) * tb.nKmax;
+    const int qm = tb.Q - 1;
+    for (int k = ka + tid; k < kb; k += nthr) {
+        const int rho = kr[k] - r0, k2 = k2s[k];
+        cx<T> acc{T(0), T(0)};
+        for (int m2 = 0; m2 < tb.Q; ++m2) {
+            const cx<T> v = d[m2 * tb.RB + rho], w = twq[(m2 * k2) & qm];
+            acc.x += v.x * w.x - v.y * w.y;
+            acc.y += v.x * w.y + v.y * w.x;
+        }
+        xn[k] = acc;
+    }
+}
+
+// Forward output i of the design operator from the needed X values.
+template <typename T>
+__device__ __forceinline__ T reg_ab_out(const RegTables<T> &tb, const cx<T> *X, int i) {
+    T r = T(0);
+    for (int t = 0; t < tb.nT; ++t) {
+        const size_t o = (size_t)t * tb.n + i;
+        const cx<T> ha = X[(size_t)t * tb.nKmax + tb.oa[o]], hb = X[(size_t)t * tb.nKmax + tb.ob[o]];
+        const cx<T> c1 = tb.oc[2 * o], c2 = tb.oc[2 * o + 1];
+        r += (c1.x * ha.x - c1.y * ha.y) + (c2.x * hb.x + c2.y * hb.y);
+    }
+    return r;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void reg_ab_finish(RegTables<T> tb, RegBufs<T> bf) {
+    const int cw = blockIdx.y;
+    const cx<T> *X = bf.xn + (size_t)cw * tb.nT * tb.nKmax;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < tb.n; i += gridDim.x * blockDim.x)
+        bf.ext_out[(size_t)cw * tb.n + i] = reg_ab_out(tb, X, i);
+}
+
+// ------------------------------------------------------------------ az stage 1
+template <typename T>
+__global__ __launch_bounds__(256) void reg_az_stage1(RegTables<T> tb, RegBufs<T> bf) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cx<T> *twq = reinterpret_cast<cx<T> *>(smem);  // [Q]
+    cx<T> *g = twq + tb.Q;                           // G of the block's needed indices
+    const int rb = blockIdx.x, t = blockIdx.y, cw = blockIdx.z;
+    if (bf.mode == 0 && !bf.active[cw]) return;
+    const int nR = tb.nR[t];
+    const int r0 = rb * tb.RB;
+    if (r0 >= nR) return;
+    const int r1 = min(nR, r0 + tb.RB), nr = r1 - r0;
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    for (int i = tid; i < tb.Q; i += nthr) twq[i] = tb.twQ[i];
+    const int32_t *kp = tb.kptr + (size_t)t * (tb.nRmax + 1);
+    const int ka = kp[r0], kb = kp[r1];
+    const T *z = (bf.mode == 0 ? bf.z : bf.ext_in) + (size_t)cw * tb.n;
+    const T phi = bf.mode == 0 ? (T)bf.phi[cw] : T(1);
+    const int32_t *gi = tb.gi + (size_t)t * tb.nKmax * 4;
+    const cx<T> *gc = tb.gc + (size_t)t * tb.nKmax * 4;
+    for (int k = ka + tid; k < kb; k += nthr) {
+        cx<T> acc{T(0), T(0)};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int i = gi[4 * k + q];
+            if (i >= 0) {
+                const T v = z[i] / phi;  // Az(z / phi), sparc.py:972
+                const cx<T> c = gc[4 * k + q];
+                acc.x += c.x * v;
+                acc.y += c.y * v;
+            }
+        }
+        g[k - ka] = acc;
+    }
+    __syncthreads();
+    const int32_t *k2s = tb.kk2 + (size_t)t * tb.nKmax, *rk = tb.row_k1 + (size_t)t * tb.nRmax;
+    cx<T> *dst = bf.tu + ((size_t)cw * tb.nT + t) * tb.Q * tb.nRmax;
+    const int qm = tb.Q - 1;
+    for (int e = tid; e < tb.Q * nr; e += nthr) {
+        const int m2 = e / nr, r = e - m2 * nr, rho = r0 + r;
+        const int a = kp[rho], b = kp[rho + 1];
+        cx<T> acc{T(0), T(0)};
+        for (int k = a; k < b; ++k) {
+            const cx<T> v = g[k - ka], w = twq[(m2 * k2s[k]) & qm];  // v * conj(w)
+            acc.x += v.x * w.x + v.y * w.y;
+            acc.y += v.y * w.x - v.x * w.y;
+        }
+        dst[(size_t)m2 * tb.nRmax + rho] = cmul(acc, cconj(reg_tw2(tb, m2, rk[rho])));
+    }
+}
+
+// ------------------------------------------------------------------ az stage 2
+template <typename T, int EPT>
+__global__ __launch_bounds__(1024) void reg_az_stage2(RegTables<T> tb, RegBufs<T> bf, int t_iter) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cx<T> *d = reinterpret_cast<cx<T> *>(smem);
+    T *dr = reinterpret_cast<T *>(smem);
+    T *sM = dr + 2 * (size_t)tb.P;
+    T *sI = sM + tb.Lblk;
+    const int m2 = blockIdx.x, t = blockIdx.y, cw = blockIdx.z;
+    if (bf.mode == 0 && !bf.active[cw]) return;
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    for (int i = tid; i < 2 * tb.P; i += nthr) dr[i] = T(0);
+    T tp = T(1), inv_tp = T(1);
+    const bool have_beta = bf.mode == 0 && t_iter > 0;
+    if (have_beta) {  // beta of the previous iteration = softmax(s_prev) with tau_prev
+        const size_t lb = (size_t)cw * tb.L + (size_t)t * tb.Lblk;
+        for (int l = tid; l < tb.Lblk; l += nthr) {
+            sM[l] = bf.stM[lb + l];
+            sI[l] = bf.stI[lb + l];
+        }
+        const double tv = bf.tau_prev[(size_t)cw * tb.Lc + t];
+        tp = (T)tv;
+        inv_tp = (T)(1.0 / tv);
+    }
+    __syncthreads();
+    const int nR = tb.nR[t];
+    const int32_t *rk = tb.row_k1 + (size_t)t * tb.nRmax;
+    const cx<T> *src = bf.tu + (((size_t)cw * tb.nT + t) * tb.Q + m2) * tb.nRmax;
+    for (int base = tid; base < nR; base += REG_CH * nthr) {
+        int k1[REG_CH];
+        cx<T> v[REG_CH];
+#pragma unroll
+        for (int i = 0; i < REG_CH; ++i) {
+            const int r = base + i * nthr;
+            if (r < nR) {
+                k1[i] = rk[r];
+                v[i] = src[r];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < REG_CH; ++i)
+            if (base + i * nthr < nR) d[k1[i]] = v[i];
+    }
+    __syncthreads();
+    lds_fft1<T, true, EPT>(d, tb.log2P, tb.stw, tid, nthr);
+    const size_t tc = (size_t)t * tb.Mc;
+    const int32_t *cp = tb.cls_ptr + (size_t)t * (tb.Q + 1);
+    const int q0 = cp[m2], q1 = cp[m2 + 1];
+    const uint16_t *loc = tb.cls_loc + tc;
+    if (bf.mode != 0) {
+        T *out = bf.ext_out + (size_t)cw * tb.LM + tc;
+        const int32_t *cj = tb.cls_j + tc;
+        for (int q = q0 + tid; q < q1; q += nthr) out[cj[q]] = dr[loc[q]];
+        return;
+    }
+    const double tv = bf.tau[(size_t)cw * tb.Lc + t];
+    const T tau = (T)tv, inv_tau = (T)(1.0 / tv);
+    T *s = bf.s + (size_t)cw * tb.LM + tc;
+    const uint16_t *sec = tb.cls_sec + tc;
+    // s = beta + tau * Az(z/phi) for the thread's entries (a class holds at
+    // most 2P = 2 EPT nthr entries); kept in registers until every u is read
+    T snv[2 * EPT];
+#pragma unroll
+    for (int c = 0; c < 2 * EPT; c += REG_CH) {
+        T v[REG_CH];
+        int lc[REG_CH], sc[REG_CH];
+#pragma unroll
+        for (int i = 0; i < REG_CH; ++i) {
+            const int q = q0 + tid + (c + i) * nthr;
+            if (q < q1) {
+                lc[i] = loc[q];
+                if (have_beta) {
+                    v[i] = s[q];
+                    sc[i] = sec[q];
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < REG_CH; ++i) {
+            const int q = q0 + tid + (c + i) * nthr;
+            if (q < q1) {
+                T b = T(0);
+                if (have_beta) b = rexp<T>(sm_arg<T>(v[i], sM[sc[i]], tp, inv_tp)) * sI[sc[i]];
+                const T sn = b + tau * dr[lc[i]];
+                s[q] = sn;
+                snv[c + i] = sn;
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 2 * EPT; ++c) {  // s of the class, contiguous in LDS (class order)
+        const int q = q0 + tid + c * nthr;
+        if (q < q1) dr[q - q0] = snv[c];
+    }
+    __syncthreads();
+    // per (class, section) statistics of the softmax, deterministic order
+    const uint16_t *sg = tb.seg + ((size_t)t * tb.Q + m2) * (tb.Lblk + 1);
+    T *pm = bf.part + (((size_t)cw * tb.nT + t) * tb.Q + m2) * 3 * (size_t)tb.Lblk;
+    for (int l = tid; l < tb.Lblk; l += nthr) {
+        const int a = sg[l], b = sg[l + 1];
+        T m = -INFINITY;
+        for (int q = a; q < b; ++q) m = fmax(m, dr[q]);
+        T S1 = T(0), S2 = T(0);
+        for (int q = a; q < b; ++q) {
+            const T e = rexp<T>(sm_arg<T>(dr[q], m, tau, inv_tau));
+            S1 += e;
+            S2 += e * e;
+        }
+        pm[l] = m;
+        pm[tb.Lblk + l] = S1;
+        pm[2 * tb.Lblk + l] = S2;
+    }
+}
+
+// ------------------------------------------------------------------ control
+// Before Az (sparc.py:931-969): Onsager residual, phi, tau.  Lr = 1.
+template <typename T>
+__global__ __launch_bounds__(256) void reg_ctrl0(RegTables<T> tb, RegBufs<T> bf, AmpScalars sc, AmpParams pr,
+                                                 int t) {
+    __shared__ double red[16];
+    __shared__ double sh_b;
+    const int cw = blockIdx.x, tid = threadIdx.x;
+    if (!bf.active[cw]) return;
+    const int Lc = tb.Lc;
+    double *psi = sc.psi + (size_t)cw * Lc, *psi_prev = sc.psi_prev + (size_t)cw * Lc;
+    double *tau = bf.tau + (size_t)cw * Lc, *tau_prev = bf.tau_prev + (size_t)cw * Lc;
+    T *z = bf.z + (size_t)cw * tb.n;
+    const T *y = bf.y + (size_t)cw * tb.n;
+    if (t > 0) {
+        if (tid == 0) {
+            for (int c = 0; c < Lc; ++c) {
+                psi_prev[c] = psi[c];
+                tau_prev[c] = tau[c];
+            }
+            sc.phi_prev[cw] = bf.phi[cw];
+            double g = 0.0;  // ndim 0: W * psi; ndim 1: dot(W, psi) / Lc
+            for (int c = 0; c < Lc; ++c) g += pr.W[c] * psi[c];
+            sc.gamma[cw] = g / Lc;
+            sc.bcoef[cw] = sc.gamma[cw] / sc.phi_prev[cw];
+            sh_b = sc.bcoef[cw];
+        }
+        __syncthreads();
+        const T b = (T)sh_b;
+        const cx<T> *X = bf.xn + (size_t)cw * tb.nT * tb.nKmax;
+        for (int i = tid; i < tb.n; i += blockDim.x) z[i] = (y[i] - reg_ab_out(tb, X, i)) + b * z[i];
+    } else {
+        for (int i = tid; i < tb.n; i += blockDim.x) z[i] = y[i];
+        if (tid == 0) {
+            double g = 0.0;
+            for (int c = 0; c < Lc; ++c) g += pr.W[c];
+            sc.gamma[cw] = g / Lc;
+        }
+    }
+    __syncthreads();
+    if (pr.phi_method == 1) {
+        if (tid == 0) bf.phi[cw] = pr.awgn_var + sc.gamma[cw];
+    } else {
+        double acc = 0.0;
+        for (int i = tid; i < tb.n; i += blockDim.x) {
+            const double v = (double)z[i];
+            acc += v * v;
+        }
+        acc = reg_block_sum(acc, red);
+        if (tid == 0) bf.phi[cw] = acc / (double)tb.n;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const double phi = bf.phi[cw];
+        for (int c = 0; c < Lc; ++c) tau[c] = (tb.L * phi / tb.n) / pr.W[c];
+    }
+}
+
+// After Az: section statistics, psi, NMSE, stopping (sparc.py:973-988).
+template <typename T>
+__global__ __launch_bounds__(1024) void reg_merge(RegTables<T> tb, RegBufs<T> bf, AmpScalars sc, AmpParams pr,
+                                                  int t) {
+    __shared__ double red[16];
+    const int cw = blockIdx.x, tid = threadIdx.x, nthr = blockDim.x;
+    if (!bf.active[cw]) return;
+    const int Lc = tb.Lc, Lb = tb.Lblk;
+    double *psi = sc.psi + (size_t)cw * Lc, *psi_prev = sc.psi_prev + (size_t)cw * Lc;
+    double *nmse = sc.nmse + (size_t)cw * pr.t_max * Lc;
+    for (int c = 0; c < Lc; ++c) {
+        const double tv = bf.tau[(size_t)cw * Lc + c];
+        const T tau = (T)tv, inv_tau = (T)(1.0 / tv);
+        const T *pm = bf.part + ((size_t)cw * tb.nT + c) * tb.Q * 3 * (size_t)Lb;
+        const T *s = bf.s + (size_t)cw * tb.LM + (size_t)c * tb.Mc;
+        double a = 0.0, e = 0.0;
+        for (int ll = tid; ll < Lb; ll += nthr) {
+            T M = -INFINITY;
+            for (int m2 = 0; m2 < tb.Q; ++m2) {
+                const T *p = pm + (size_t)m2 * 3 * Lb;
+                if (p[Lb + ll] > T(0)) M = fmax(M, p[ll]);
+            }
+            T S1 = T(0), S2 = T(0);
+            for (int m2 = 0; m2 < tb.Q; ++m2) {
+                const T *p = pm + (size_t)m2 * 3 * Lb;
+                const T S = p[Lb + ll];
+                if (S > T(0)) {
+                    const T f = rexp<T>(sm_arg<T>(p[ll], M, tau, inv_tau));
+                    S1 += S * f;
+                    S2 += p[2 * Lb + ll] * (f * f);
+                }
+            }
+            const int l = c * Lb + ll;
+            const T inv = T(1) / S1;
+            bf.stM[(size_t)cw * tb.L + l] = M;
+            bf.stI[(size_t)cw * tb.L + l] = inv;
+            const double ss = (double)(S2 * inv * inv);
+            double err = ss;
+            if (bf.true_idx) {
+                const int jl = ll * tb.M + bf.true_idx[(size_t)cw * tb.L + l];
+                const int q = tb.qpos[(size_t)c * tb.Mc + jl];
+                const double bt = (double)(rexp<T>(sm_arg<T>(s[q], M, tau, inv_tau)) * inv);
+                err = ss - 2.0 * bt + 1.0;
+            }
+            a += ss;
+            e += err;
+        }
+        a = reg_block_sum(a, red);
+        e = reg_block_sum(e, red);
+        if (tid == 0) {
+            const double denom = (Lc == 1) ? (double)tb.L : (double)Lb;
+            psi[c] = 1.0 - a / denom;
+            nmse[(size_t)(t + 1) * Lc + c] = e / denom;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        bool stop = false;
+        if (t > 0) {
+            stop = true;
+            for (int c = 0; c < Lc; ++c)
+                if (!(fabs(psi[c] - psi_prev[c]) <= pr.atol + pr.rtol * fabs(psi_prev[c]))) stop = false;
+        }
+        if (stop) {  // nmse[t:] = nmse[t] (sparc.py:985)
+            for (int tt = t + 1; tt < pr.t_max; ++tt)
+                for (int c = 0; c < Lc; ++c) nmse[(size_t)tt * Lc + c] = nmse[(size_t)t * Lc + c];
+            sc.t_final[cw] = t + 1;
+            bf.active[cw] = 0;
+        } else if (t == pr.t_max - 2) {
+            sc.t_final[cw] = t + 1;
+            bf.active[cw] = 0;
+        }
+    }
+}
+
+// Final MAP decision (sparc.py:997, msg_vector_map_estimator :485-487): the
+// first index of each section where s attains the section maximum.
+template <typename T>
+__global__ __launch_bounds__(256) void reg_map(RegTables<T> tb, RegBufs<T> bf) {
+    const int m2 = blockIdx.x, t = blockIdx.y, cw = blockIdx.z;
+    const size_t tc = (size_t)t * tb.Mc;
+    const int32_t *cp = tb.cls_ptr + (size_t)t * (tb.Q + 1);
+    const int q0 = cp[m2], q1 = cp[m2 + 1];
+    const T *s = bf.s + (size_t)cw * tb.LM + tc;
+    const uint16_t *sec = tb.cls_sec + tc;
+    const int32_t *cj = tb.cls_j + tc;
+    for (int q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
+        const int ls = sec[q];
+        const size_t l = (size_t)cw * tb.L + (size_t)t * tb.Lblk + ls;
+        if (s[q] == bf.stM[l]) atomicMin(&bf.map[l], cj[q] - ls * tb.M);
+    }
+}
+
+// Initial state (sparc.py:914-927): every codeword active, nmse[0..] = 1.
+__global__ void reg_init_kernel(int Lc, int t_max, double *nmse, int32_t *active, int32_t *t_final) {
+    const int cw = blockIdx.x;
+    for (int i = threadIdx.x; i < t_max * Lc; i += blockDim.x) nmse[(size_t)cw * t_max * Lc + i] = 1.0;
+    if (threadIdx.x == 0) {
+        active[cw] = 1;
+        t_final[cw] = 0;
+    }
+}
+
+int reg_launch_init(int B, int Lc, int t_max, double *nmse, int32_t *active, int32_t *t_final, hipStream_t s) {
+    if (B <= 0) return SG_OK;
+    hipLaunchKernelGGL(reg_init_kernel, dim3(B), dim3(256), 0, s, Lc, t_max, nmse, active, t_final);
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
+// ------------------------------------------------------------------ launchers
+template <typename T>
+static int reg_ept(int P) {
+    const int e = P / 1024;
+    return e > 8 ? e : 8;
+}
+
+template <typename T, int EPT>
+static void launch_s1(const RegTables<T> &tb, const RegBufs<T> &bf, size_t lds, hipStream_t s) {
+    hipLaunchKernelGGL((reg_ab_stage1<T, EPT>), dim3(tb.Q, tb.nT, bf.B), dim3(tb.P / EPT), lds, s, tb, bf);
+}
+template <typename T, int EPT>
+static void launch_s2i(const RegTables<T> &tb, const RegBufs<T> &bf, int t_iter, size_t lds, hipStream_t s) {
+    hipLaunchKernelGGL((reg_az_stage2<T, EPT>), dim3(tb.Q, tb.nT, bf.B), dim3(tb.P / EPT), lds, s, tb, bf,
+                       t_iter);
+}
+
+template <typename T>
+static int reg_set_attrs() {
+    static bool done = false;
+    if (done) return SG_OK;
+    const int mx = 160 * 1024;
+#define SG_LDS_ATTR(K) SG_HIP(hipFuncSetAttribute((const void *)(K), hipFuncAttributeMaxDynamicSharedMemorySize, mx))
+    SG_LDS_ATTR((reg_ab_stage1<T, 8>)); SG_LDS_ATTR((reg_ab_stage1<T, 16>));
+    SG_LDS_ATTR((reg_az_stage2<T, 8>)); SG_LDS_ATTR((reg_az_stage2<T, 16>));
+    SG_LDS_ATTR((reg_ab_stage2<T>)); SG_LDS_ATTR((reg_az_stage1<T>));
+#undef SG_LDS_ATTR
+    done = true;
+    return SG_OK;
+}
+
+template <typename T>
+int reg_launch_ab(const RegTables<T> &tb, const RegBufs<T> &bf, hipStream_t s) {
+    if (bf.B <= 0) return SG_OK;
+    SG_TRY(reg_set_attrs<T>());
+    const size_t lds1 = reg_stage1_lds(tb.P, tb.Lblk, sizeof(T));
+    const int ept = reg_ept<T>(tb.P);
+    {
+        ProfScope ps(SG_PH_AB_A, s);
+        if (ept == 8) launch_s1<T, 8>(tb, bf, lds1, s);
+        else if (ept == 16) launch_s1<T, 16>(tb, bf, lds1, s);
+        else return fail(SG_ERR_UNSUPPORTED, "stage-1 FFT length P=%d unsupported", tb.P);
+    }
+    SG_HIP(hipGetLastError());
+    {
+        ProfScope ps(SG_PH_AB_B, s);
+        const size_t lds2 = sizeof(cx<T>) * ((size_t)tb.Q * tb.RB + tb.Q);
+        hipLaunchKernelGGL((reg_ab_stage2<T>), dim3(tb.nrb, tb.nT, bf.B), dim3(256), lds2, s, tb, bf);
+    }
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
+template <typename T>
+int reg_launch_ab_finish(const RegTables<T> &tb, const RegBufs<T> &bf, hipStream_t s) {
+    if (bf.B <= 0) return SG_OK;
+    hipLaunchKernelGGL((reg_ab_finish<T>), dim3((tb.n + 255) / 256, bf.B), dim3(256), 0, s, tb, bf);
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
+template <typename T>
+int reg_launch_az(const RegTables<T> &tb, const RegBufs<T> &bf, int t_iter, hipStream_t s) {
+    if (bf.B <= 0) return SG_OK;
+    SG_TRY(reg_set_attrs<T>());
+    {
+        ProfScope ps(SG_PH_AZ_A, s);
+        const size_t ldsg = sizeof(cx<T>) * ((size_t)(tb.maxKb > 0 ? tb.maxKb : 1) + tb.Q);
+        hipLaunchKernelGGL((reg_az_stage1<T>), dim3(tb.nrb, tb.nT, bf.B), dim3(256), ldsg, s, tb, bf);
+    }
+    SG_HIP(hipGetLastError());
+    const size_t lds1 = reg_stage1_lds(tb.P, tb.Lblk, sizeof(T));
+    const int ept = reg_ept<T>(tb.P);
+    {
+        ProfScope ps(SG_PH_AZ_B, s);
+        if (ept == 8) launch_s2i<T, 8>(tb, bf, t_iter, lds1, s);
+        else if (ept == 16) launch_s2i<T, 16>(tb, bf, t_iter, lds1, s);
+        else return fail(SG_ERR_UNSUPPORTED, "stage-1 FFT length P=%d unsupported", tb.P);
+    }
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
+template <typename T>
+int reg_launch_ctrl0(const RegTables<T> &tb, const RegBufs<T> &bf, const AmpScalars &sc, const AmpParams &pr, int t,
+                     hipStream_t s) {
+    if (bf.B <= 0) return SG_OK;
+    ProfScope ps(SG_PH_CONTROL, s);
+    hipLaunchKernelGGL((reg_ctrl0<T>), dim3(bf.B), dim3(256), 0, s, tb, bf, sc, pr, t);
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
+template <typename T>
+int reg_launch_merge(const RegTables<T> &tb, const RegBufs<T> &bf, const AmpScalars &sc, const AmpParams &pr, int t,
+                     hipStream_t s) {
+    if (bf.B <= 0) return SG_OK;
+    ProfScope ps(SG_PH_ETA, s);
+    hipLaunchKernelGGL((reg_merge<T>), dim3(bf.B), dim3(1024), 0, s, tb, bf, sc, pr, t);
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
+template <typename T>
+int reg_launch_map(const RegTables<T> &tb, const RegBufs<T> &bf, hipStream_t s) {
+    if (bf.B <= 0) return SG_OK;
+    hipLaunchKernelGGL((reg_map<T>), dim3(tb.Q, tb.nT, bf.B), dim3(256), 0, s, tb, bf);
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
+#define SG_REG_INST(T)                                                                                          \
+    template int reg_launch_ab<T>(const RegTables<T> &, const RegBufs<T> &, hipStream_t);                       \
+    template int reg_launch_az<T>(const RegTables<T> &, const RegBufs<T> &, int, hipStream_t);                  \
+    template int reg_launch_ctrl0<T>(const RegTables<T> &, const RegBufs<T> &, const AmpScalars &,             \
+                                     const AmpParams &, int, hipStream_t);                                     \
+    template int reg_launch_merge<T>(const RegTables<T> &, const RegBufs<T> &, const AmpScalars &,             \
+                                     const AmpParams &, int, hipStream_t);                                     \
+    template int reg_launch_map<T>(const RegTables<T> &, const RegBufs<T> &, hipStream_t);                      \
+    template int reg_launch_ab_finish<T>(const RegTables<T> &, const RegBufs<T> &, hipStream_t);
+SG_REG_INST(float)
+SG_REG_INST(double)
+
+}  // namespace sg

@@ -1,6 +1,8 @@
 // C ABI of the AMP decoder: design plans (sub-sampled DCT operator tables),
 // batched decode, the design operators Ab / Az, error counting.
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <cmath>
 #include <complex>
 #include <memory>
@@ -33,6 +35,18 @@ struct sg_amp_plan {
     double *ws_psi = nullptr, *ws_psi_prev = nullptr, *ws_phi_prev = nullptr, *ws_gamma = nullptr, *ws_bco = nullptr;
     double *ws_nmse = nullptr;
     int32_t *ws_active = nullptr, *ws_argmax = nullptr, *ws_true = nullptr, *ws_tfinal = nullptr;
+    // regular engine (one transform per column block, amp_fused.hip)
+    bool regular = false;
+    int rP = 0, rQ = 0, rlog2P = 0, nRmax = 0, nKmax = 0, RB = 0, nrb = 0, maxKb = 0, Lblk = 0, nB = 0;
+    int32_t *r_nR = nullptr, *r_row_k1 = nullptr, *r_kptr = nullptr, *r_kk2 = nullptr, *r_krho = nullptr;
+    int32_t *r_oa = nullptr, *r_ob = nullptr, *r_gi = nullptr, *r_cls_ptr = nullptr, *r_cls_j = nullptr,
+            *r_qpos = nullptr;
+    uint16_t *r_cls_loc = nullptr, *r_cls_sec = nullptr, *r_seg = nullptr;
+    void *r_oc = nullptr, *r_gc = nullptr, *r_twP = nullptr, *r_twQ = nullptr, *r_stw = nullptr, *r_twa = nullptr,
+         *r_twb = nullptr;
+    void *ws_s = nullptr, *ws_tu = nullptr, *ws_xn = nullptr, *ws_part = nullptr, *ws_stM = nullptr,
+         *ws_stI = nullptr;
+    double *ws_tau_prev = nullptr;
 };
 
 extern "C" int sg_amp_plan_destroy(sg_amp_plan *p);
@@ -81,12 +95,52 @@ static cd tw(long long k, long long m) {
     return expi(-2.0 * M_PI * (double)k / (double)m);
 }
 
+// Forward output at DCT position k (sparc.py:687-692 via the Makhoul packed
+// FFT): X_dct[k] = Re(c1 H[a] + c2 conj(H[b])), H = FFT_{N/2} of the packed
+// sequence; sc = sqrt(W/L) of the block (sparc.py:786-794).
+static void fwd_coef(long long k, long long N, long long N2, double sc, long long *a, long long *b, cd *c1, cd *c2) {
+    const long long kk = (k <= N2) ? k : N - k;
+    *a = kk % N2;
+    *b = (N2 - kk) % N2;
+    const cd e = (k <= N2) ? expi(-M_PI * (double)k / (2.0 * N)) : expi(M_PI * (double)k / (2.0 * N));
+    const cd wk = tw(kk, N);
+    const cd I(0, 1);
+    const double sqrt2 = std::sqrt(2.0);
+    *c1 = e * (0.5 - 0.5 * I * wk) * (sqrt2 * sc);
+    *c2 = e * (0.5 + 0.5 * I * wk) * (sqrt2 * sc);
+}
+
+// Inverse input: a value v at DCT position q (sparc.py:694-699) contributes
+// coef * v to the packed spectrum G at one or two N/2-indices:
+// G[k] = A_k y[k] - i A_k y[N-k] + C_k y[N2+k] - i C_k y[N2-k].
+template <typename F>
+static void inv_contrib(long long q, long long N, long long N2, double sc, F &&add) {
+    const cd I(0, 1);
+    auto Ak = [&](long long k) { return expi(M_PI * (double)k / (2.0 * N)) * (1.0 + I * tw(-k, N)); };
+    auto Ck = [&](long long k) { return expi(M_PI * (double)(k + N2) / (2.0 * N)) * (1.0 - I * tw(-k, N)); };
+    const double gsc = sc / std::sqrt(2.0);  // sqrt(2 W/L) * (1/2)
+    if (q < N2) {
+        add(q, Ak(q) * gsc);
+        add(N2 - q, -I * Ck(N2 - q) * gsc);
+    } else if (q > N2) {
+        add(N - q, -I * Ak(N - q) * gsc);
+        add(q - N2, Ck(q - N2) * gsc);
+    } else {
+        add(0, Ck(0) * (1.0 - I) * gsc);
+    }
+}
+
+static long long slot_of_pos(long long pos, long long N) {  // w-space slot of DCT position pos
+    return (pos % 2 == 0) ? pos / 2 : N - 1 - (pos - 1) / 2;
+}
+
 static int plan_free_ws(sg_amp_plan *p) {
     void **ws[] = {&p->ws_beta, &p->ws_y, &p->ws_z, &p->ws_rbuf, &p->ws_buf0, &p->ws_buf1, &p->ws_io,
                    (void **)&p->ws_phi, (void **)&p->ws_tau, (void **)&p->ws_sumsq, (void **)&p->ws_err,
                    (void **)&p->ws_psi, (void **)&p->ws_psi_prev, (void **)&p->ws_phi_prev, (void **)&p->ws_gamma,
                    (void **)&p->ws_bco, (void **)&p->ws_nmse, (void **)&p->ws_active, (void **)&p->ws_argmax,
-                   (void **)&p->ws_true, (void **)&p->ws_tfinal};
+                   (void **)&p->ws_true, (void **)&p->ws_tfinal, &p->ws_s, &p->ws_tu, &p->ws_xn, &p->ws_part,
+                   &p->ws_stM, &p->ws_stI, (void **)&p->ws_tau_prev};
     for (void **x : ws) {
         if (*x) hipFree(*x);
         *x = nullptr;
@@ -103,16 +157,26 @@ static int ensure_ws(sg_amp_plan *p, int B, int t_max) {
     const size_t rs = p->precision == SG_F64 ? 8 : 4;
     const size_t Bz = (size_t)B;
 #define SG_ALLOC(ptr, bytes) SG_HIP(hipMalloc((void **)&(ptr), std::max<size_t>(16, (bytes))))
-    SG_ALLOC(p->ws_beta, Bz * p->LM * rs);
     SG_ALLOC(p->ws_y, Bz * p->n * rs);
     SG_ALLOC(p->ws_z, Bz * p->n * rs);
-    SG_ALLOC(p->ws_rbuf, Bz * p->nT * p->Mr * rs);
-    SG_ALLOC(p->ws_buf0, Bz * p->nT * p->N2 * 2 * rs);
-    SG_ALLOC(p->ws_buf1, Bz * p->nT * p->N2 * 2 * rs);
+    if (p->regular) {
+        SG_ALLOC(p->ws_s, Bz * p->LM * rs);
+        SG_ALLOC(p->ws_tu, Bz * p->nT * p->rQ * p->nRmax * 2 * rs);
+        SG_ALLOC(p->ws_xn, Bz * p->nT * p->nKmax * 2 * rs);
+        SG_ALLOC(p->ws_part, Bz * p->nT * p->rQ * 3 * p->Lblk * rs);
+        SG_ALLOC(p->ws_stM, Bz * p->L * rs);
+        SG_ALLOC(p->ws_stI, Bz * p->L * rs);
+        SG_ALLOC(p->ws_tau_prev, Bz * p->Lc * 8);
+    } else {
+        SG_ALLOC(p->ws_beta, Bz * p->LM * rs);
+        SG_ALLOC(p->ws_rbuf, Bz * p->nT * p->Mr * rs);
+        SG_ALLOC(p->ws_buf0, Bz * p->nT * p->N2 * 2 * rs);
+        SG_ALLOC(p->ws_buf1, Bz * p->nT * p->N2 * 2 * rs);
+        SG_ALLOC(p->ws_sumsq, Bz * p->L * 8);
+        SG_ALLOC(p->ws_err, Bz * p->L * 8);
+    }
     SG_ALLOC(p->ws_phi, Bz * p->Lr * 8);
     SG_ALLOC(p->ws_tau, Bz * p->Lc * 8);
-    SG_ALLOC(p->ws_sumsq, Bz * p->L * 8);
-    SG_ALLOC(p->ws_err, Bz * p->L * 8);
     SG_ALLOC(p->ws_psi, Bz * p->Lc * 8);
     SG_ALLOC(p->ws_psi_prev, Bz * p->Lc * 8);
     SG_ALLOC(p->ws_phi_prev, Bz * p->Lr * 8);
@@ -151,6 +215,236 @@ static AmpBufs<T> bufs(const sg_amp_plan *p, int B, const void *y) {
     bf.buf0 = (cx<T> *)p->ws_buf0; bf.buf1 = (cx<T> *)p->ws_buf1; bf.phi = p->ws_phi; bf.tau = p->ws_tau;
     bf.active = p->ws_active; bf.sec_sumsq = p->ws_sumsq; bf.sec_err = p->ws_err; bf.sec_argmax = p->ws_argmax;
     bf.true_idx = nullptr;
+    return bf;
+}
+
+// Tables of the regular engine (amp_fused.hip), one transform per column
+// block: class order of each block's entries and the needed-row structure of
+// the two FFT stages.  Sizes: P = stage-1 FFT length (LDS resident), Q = N2/P.
+static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t *order1,
+                         const std::vector<double> &t_scale) {
+    const long long N = p->w, N2 = p->N2;
+    const int nT = p->nT, Mc = p->Mc, n = p->n, M = p->M;
+    const int Lblk = p->L / p->Lc;
+    SG_CHECK_ARG(Lblk < 65536, "too many sections per column block (%d)", Lblk);
+    const size_t rb = p->precision == SG_F64 ? 8 : 4;
+    int P = (int)std::min<long long>(N2, p->precision == SG_F64 ? 8192 : 16384);
+    while (P > 8 && reg_stage1_lds(P, Lblk, rb) > 160 * 1024) P >>= 1;
+    SG_CHECK_ARG(reg_stage1_lds(P, Lblk, rb) <= 160 * 1024, "section statistics exceed the LDS budget");
+    const int Q = (int)(N2 / P);
+    p->rP = P; p->rQ = Q; p->rlog2P = ilog2(P); p->Lblk = Lblk;
+    const size_t cxb = 2 * rb;
+    p->RB = (int)std::min<size_t>(256, std::max<size_t>(1, 65536 / ((size_t)Q * cxb)));
+
+    std::vector<std::vector<int32_t>> row_k1(nT), kptr(nT), kk2(nT), krho(nT), oa(nT), ob(nT), gi(nT);
+    std::vector<std::vector<cd>> oc(nT), gc(nT);
+    std::vector<int32_t> cls_ptr((size_t)nT * (Q + 1)), cls_j((size_t)nT * Mc), qpos((size_t)nT * Mc);
+    std::vector<uint16_t> cls_loc((size_t)nT * Mc), cls_sec((size_t)nT * Mc), seg((size_t)nT * Q * (Lblk + 1));
+    std::vector<int32_t> kidx(N2, -1);
+    std::vector<uint8_t> used(N), need(N2);
+    for (int t = 0; t < nT; ++t) {
+        const uint32_t *o0 = order0 + (size_t)t * n, *o1 = order1 + (size_t)t * Mc;
+        // ---- class order of the column block: (class m2, section, j)
+        std::fill(used.begin(), used.end(), 0);
+        std::vector<int32_t> cnt(Q + 1, 0), m2of(Mc), locof(Mc);
+        for (int j = 0; j < Mc; ++j) {
+            const long long pos = o1[j];
+            SG_CHECK_ARG(pos >= 1 && pos < N, "order1 entry %lld outside [1, w)", pos);
+            const long long sl = slot_of_pos(pos, N);
+            SG_CHECK_ARG(!used[sl], "order1 has a repeated position");
+            used[sl] = 1;
+            const long long m = sl >> 1;
+            m2of[j] = (int)(m % Q);
+            locof[j] = (int)(2 * (m / Q) + (sl & 1));
+            cnt[m2of[j] + 1]++;
+        }
+        int32_t *cpt = cls_ptr.data() + (size_t)t * (Q + 1);
+        cpt[0] = 0;
+        for (int c = 0; c < Q; ++c) cpt[c + 1] = cpt[c] + cnt[c + 1];
+        std::vector<int32_t> fill(cpt, cpt + Q);
+        for (int j = 0; j < Mc; ++j) {  // ascending j: each class sorted by (section, j)
+            const int q = fill[m2of[j]]++;
+            const size_t o = (size_t)t * Mc + q;
+            cls_loc[o] = (uint16_t)locof[j];
+            cls_sec[o] = (uint16_t)(j / M);
+            cls_j[o] = j;
+            qpos[(size_t)t * Mc + j] = q;
+        }
+        for (int c = 0; c < Q; ++c) {
+            uint16_t *sg = seg.data() + ((size_t)t * Q + c) * (Lblk + 1);
+            const int q0 = cpt[c], q1 = cpt[c + 1];
+            int q = q0;
+            for (int l = 0; l <= Lblk; ++l) {
+                while (q < q1 && cls_sec[(size_t)t * Mc + q] < l) ++q;
+                sg[l] = (uint16_t)(q - q0);
+            }
+        }
+        // ---- needed N/2-indices: forward outputs = inverse inputs
+        std::fill(need.begin(), need.end(), 0);
+        std::fill(used.begin(), used.end(), 0);
+        for (int i = 0; i < n; ++i) {
+            const long long k = o0[i];
+            SG_CHECK_ARG(k >= 1 && k < N, "order0 entry %lld outside [1, w)", k);
+            SG_CHECK_ARG(!used[k], "order0 has a repeated position");
+            used[k] = 1;
+            const long long kk = (k <= N2) ? k : N - k;
+            need[kk % N2] = 1;
+            need[(N2 - kk) % N2] = 1;
+        }
+        int nk = 0;
+        for (int k1 = 0; k1 < P; ++k1) {
+            bool any = false;
+            for (int k2 = 0; k2 < Q; ++k2) {
+                const long long idx = k1 + (long long)P * k2;
+                if (!need[idx]) continue;
+                if (!any) {
+                    row_k1[t].push_back(k1);
+                    kptr[t].push_back(nk);
+                    any = true;
+                }
+                kk2[t].push_back(k2);
+                krho[t].push_back((int)row_k1[t].size() - 1);
+                kidx[idx] = nk++;
+            }
+        }
+        kptr[t].push_back(nk);
+        oa[t].resize(n);
+        ob[t].resize(n);
+        oc[t].resize(2 * (size_t)n);
+        for (int i = 0; i < n; ++i) {
+            long long a, b;
+            cd c1, c2;
+            fwd_coef(o0[i], N, N2, t_scale[t], &a, &b, &c1, &c2);
+            oa[t][i] = kidx[a];
+            ob[t][i] = kidx[b];
+            oc[t][2 * i] = c1;
+            oc[t][2 * i + 1] = c2;
+        }
+        gi[t].assign(4 * (size_t)nk, -1);
+        gc[t].assign(4 * (size_t)nk, cd(0, 0));
+        std::vector<int> ng(nk, 0);
+        bool ok = true;
+        for (int i = 0; i < n; ++i)
+            inv_contrib(o0[i], N, N2, t_scale[t], [&](long long k, cd c) {
+                const int kx = kidx[k];
+                if (kx < 0 || ng[kx] >= 4) { ok = false; return; }
+                gi[t][4 * (size_t)kx + ng[kx]] = i;
+                gc[t][4 * (size_t)kx + ng[kx]] = c;
+                ng[kx]++;
+            });
+        SG_CHECK_ARG(ok, "internal: inverse contribution outside the needed set");
+        for (int i = 0; i < n; ++i) {  // reset the index map for the next transform
+            const long long k = o0[i], kk = (k <= N2) ? k : N - k;
+            kidx[kk % N2] = -1;
+            kidx[(N2 - kk) % N2] = -1;
+        }
+    }
+    int nRmax = 1, nKmax = 1;
+    for (int t = 0; t < nT; ++t) {
+        nRmax = std::max(nRmax, (int)row_k1[t].size());
+        nKmax = std::max(nKmax, (int)kk2[t].size());
+    }
+    p->nRmax = nRmax; p->nKmax = nKmax;
+    p->nrb = (nRmax + p->RB - 1) / p->RB;
+    std::vector<int32_t> nR(nT), f_rk((size_t)nT * nRmax, 0), f_kp((size_t)nT * (nRmax + 1), 0);
+    std::vector<int32_t> f_k2((size_t)nT * nKmax, 0), f_kr((size_t)nT * nKmax, 0), f_oa((size_t)nT * n),
+        f_ob((size_t)nT * n), f_gi((size_t)nT * nKmax * 4, -1);
+    std::vector<cd> f_oc((size_t)nT * n * 2), f_gc((size_t)nT * nKmax * 4, cd(0, 0));
+    int maxKb = 0;
+    for (int t = 0; t < nT; ++t) {
+        const int r = (int)row_k1[t].size(), k = (int)kk2[t].size();
+        nR[t] = r;
+        std::copy(row_k1[t].begin(), row_k1[t].end(), f_rk.begin() + (size_t)t * nRmax);
+        for (int i = 0; i <= nRmax; ++i) f_kp[(size_t)t * (nRmax + 1) + i] = kptr[t][std::min(i, r)];
+        std::copy(kk2[t].begin(), kk2[t].end(), f_k2.begin() + (size_t)t * nKmax);
+        std::copy(krho[t].begin(), krho[t].end(), f_kr.begin() + (size_t)t * nKmax);
+        std::copy(oa[t].begin(), oa[t].end(), f_oa.begin() + (size_t)t * n);
+        std::copy(ob[t].begin(), ob[t].end(), f_ob.begin() + (size_t)t * n);
+        std::copy(oc[t].begin(), oc[t].end(), f_oc.begin() + (size_t)t * n * 2);
+        std::copy(gi[t].begin(), gi[t].end(), f_gi.begin() + (size_t)t * nKmax * 4);
+        std::copy(gc[t].begin(), gc[t].end(), f_gc.begin() + (size_t)t * nKmax * 4);
+        for (int b = 0; b * p->RB < r; ++b)
+            maxKb = std::max(maxKb, kptr[t][std::min(r, (b + 1) * p->RB)] - kptr[t][b * p->RB]);
+        (void)k;
+    }
+    p->maxKb = maxKb;
+    std::vector<cd> twP(P), twQ(Q);
+    for (int i = 0; i < P; ++i) twP[i] = tw(i, P);
+    for (int i = 0; i < Q; ++i) twQ[i] = tw(i, Q);
+    // per-stage twiddles of the P-point FFT in thread order (fft.hpp lds_fft1)
+    std::vector<cd> stw;
+    {
+        int n2, n4, n8;
+        fft1_plan(p->rlog2P, &n2, &n4, &n8);
+        int lns = 0;
+        auto stage = [&](int R, int LR) {
+            const long long Ns = 1LL << lns;
+            for (long long k = 0; k < Ns; ++k)
+                for (int r = 1; r < R; ++r) stw.push_back(tw(r * k, Ns * R));
+            lns += LR;
+        };
+        for (int i = 0; i < n2; ++i) stage(2, 1);
+        for (int i = 0; i < n4; ++i) stage(4, 2);
+        for (int i = 0; i < n8; ++i) stage(8, 3);
+        if (stw.empty()) stw.push_back(cd(1, 0));
+    }
+    const int nB = (P + 63) / 64;
+    p->nB = nB;
+    std::vector<cd> twa((size_t)Q * 64), twb((size_t)Q * nB);
+    for (int m2 = 0; m2 < Q; ++m2) {
+        for (int a = 0; a < 64; ++a) twa[(size_t)m2 * 64 + a] = tw((long long)m2 * a, N2);
+        for (int b = 0; b < nB; ++b) twb[(size_t)m2 * nB + b] = tw((long long)m2 * 64 * b, N2);
+    }
+    SG_TRY(upload(p, &p->r_nR, nR));
+    SG_TRY(upload(p, &p->r_row_k1, f_rk));
+    SG_TRY(upload(p, &p->r_kptr, f_kp));
+    SG_TRY(upload(p, &p->r_kk2, f_k2));
+    SG_TRY(upload(p, &p->r_krho, f_kr));
+    SG_TRY(upload(p, &p->r_oa, f_oa));
+    SG_TRY(upload(p, &p->r_ob, f_ob));
+    SG_TRY(upload_cx(p, &p->r_oc, f_oc));
+    SG_TRY(upload(p, &p->r_gi, f_gi));
+    SG_TRY(upload_cx(p, &p->r_gc, f_gc));
+    SG_TRY(upload(p, &p->r_cls_ptr, cls_ptr));
+    SG_TRY(upload(p, &p->r_cls_loc, cls_loc));
+    SG_TRY(upload(p, &p->r_cls_sec, cls_sec));
+    SG_TRY(upload(p, &p->r_cls_j, cls_j));
+    SG_TRY(upload(p, &p->r_qpos, qpos));
+    SG_TRY(upload(p, &p->r_seg, seg));
+    SG_TRY(upload_cx(p, &p->r_twP, twP));
+    SG_TRY(upload_cx(p, &p->r_twQ, twQ));
+    SG_TRY(upload_cx(p, &p->r_stw, stw));
+    SG_TRY(upload_cx(p, &p->r_twa, twa));
+    SG_TRY(upload_cx(p, &p->r_twb, twb));
+    return SG_OK;
+}
+
+template <typename T>
+static RegTables<T> rtables(const sg_amp_plan *p) {
+    RegTables<T> tb;
+    tb.nT = p->nT; tb.L = p->L; tb.M = p->M; tb.LM = p->LM; tb.n = p->n; tb.Lc = p->Lc; tb.Mc = p->Mc;
+    tb.Lblk = p->Lblk; tb.N2 = p->N2; tb.P = p->rP; tb.Q = p->rQ; tb.log2P = p->rlog2P;
+    tb.nRmax = p->nRmax; tb.nKmax = p->nKmax; tb.RB = p->RB; tb.nrb = p->nrb; tb.maxKb = p->maxKb;
+    tb.nR = p->r_nR; tb.row_k1 = p->r_row_k1; tb.kptr = p->r_kptr; tb.kk2 = p->r_kk2; tb.krho = p->r_krho;
+    tb.oa = p->r_oa; tb.ob = p->r_ob; tb.oc = (const cx<T> *)p->r_oc; tb.gi = p->r_gi; tb.gc = (const cx<T> *)p->r_gc;
+    tb.cls_ptr = p->r_cls_ptr; tb.cls_loc = p->r_cls_loc; tb.cls_sec = p->r_cls_sec; tb.cls_j = p->r_cls_j;
+    tb.qpos = p->r_qpos; tb.seg = p->r_seg;
+    tb.twP = (const cx<T> *)p->r_twP; tb.twQ = (const cx<T> *)p->r_twQ;
+    tb.twHi = (const cx<T> *)p->twHi; tb.twLo = (const cx<T> *)p->twLo;
+    tb.stw = (const cx<T> *)p->r_stw; tb.twa = (const cx<T> *)p->r_twa; tb.twb = (const cx<T> *)p->r_twb;
+    tb.nB = p->nB;
+    return tb;
+}
+
+template <typename T>
+static RegBufs<T> rbufs(const sg_amp_plan *p, int B, const void *y) {
+    RegBufs<T> bf;
+    bf.B = B; bf.mode = 0;
+    bf.s = (T *)p->ws_s; bf.tu = (cx<T> *)p->ws_tu; bf.xn = (cx<T> *)p->ws_xn; bf.part = (T *)p->ws_part;
+    bf.stM = (T *)p->ws_stM; bf.stI = (T *)p->ws_stI;
+    bf.y = (const T *)(y ? y : p->ws_y); bf.z = (T *)p->ws_z;
+    bf.phi = p->ws_phi; bf.tau = p->ws_tau; bf.tau_prev = p->ws_tau_prev; bf.active = p->ws_active;
+    bf.true_idx = nullptr; bf.map = p->ws_argmax; bf.ext_in = nullptr; bf.ext_out = nullptr;
     return bf;
 }
 
@@ -202,6 +496,13 @@ static int build_plan(int ndim, const double *W, int Lr_in, int Lc_in, int L, in
             if (t_col[t] == c) col_t.push_back(t);
         col_ptr[c + 1] = (int32_t)col_t.size();
     }
+    // one transform per column block: the regular engine (amp_fused.hip);
+    // SG_AMP_ENGINE=legacy keeps the general four-step path for comparison
+    const char *eng = std::getenv("SG_AMP_ENGINE");
+    // (the per-section softmax statistics of a column block must fit in LDS
+    // beside the stage-1 FFT: at most 2048 (f64) / 4096 (f32) sections)
+    const size_t sec_bytes = (size_t)2 * (L / Lc) * (precision == SG_F64 ? 8 : 4);
+    p->regular = ndim <= 1 && p->nT == Lc && sec_bytes <= 32 * 1024 && !(eng && std::strcmp(eng, "legacy") == 0);
     const int N = w, N2 = p->N2, P = p->P, Q = p->Q, np1 = p->npairs + 1;
     auto slot_of = [&](long long pos) -> long long {  // w-space slot of position pos
         return (pos % 2 == 0) ? pos / 2 : (long long)N - 1 - (pos - 1) / 2;
@@ -222,8 +523,7 @@ static int build_plan(int ndim, const double *W, int Lr_in, int Lc_in, int L, in
     std::vector<cd> rp_c;
     std::vector<int32_t> gs_ptr((size_t)p->nT * np1), gs_loc, gs_i;
     std::vector<cd> gs_c;
-    const double sqrt2 = std::sqrt(2.0);
-    for (int t = 0; t < p->nT; ++t) {
+    for (int t = 0; t < p->nT && !p->regular; ++t) {
         const uint32_t *o0 = order0 + (size_t)t * Mr, *o1 = order1 + (size_t)t * Mc;
         int32_t *im = inmap.data() + (size_t)t * N;
         for (int j = 0; j < Mc; ++j) {
@@ -249,14 +549,9 @@ static int build_plan(int ndim, const double *W, int Lr_in, int Lc_in, int L, in
         for (int pr = 0; pr < p->npairs; ++pr) {
             rp_ptr[(size_t)t * np1 + pr] = (int32_t)rp_i.size();
             for (int i : by_pair[pr]) {
-                const long long k = o0[i];
-                const long long kk = (k <= N2) ? k : N - k;
-                const long long a = kk % N2, b = (N2 - kk) % N2;
-                const cd e = (k <= N2) ? expi(-M_PI * (double)k / (2.0 * N)) : expi(M_PI * (double)k / (2.0 * N));
-                const cd wk = tw(kk, N);
-                const cd I(0, 1);
-                const cd c1 = e * (0.5 - 0.5 * I * wk) * (sqrt2 * sc);
-                const cd c2 = e * (0.5 + 0.5 * I * wk) * (sqrt2 * sc);
+                long long a, b;
+                cd c1, c2;
+                fwd_coef(o0[i], N, N2, sc, &a, &b, &c1, &c2);
                 rp_i.push_back(i);
                 rp_ab.push_back(local_of(a) | (local_of(b) << 16));
                 rp_c.push_back(c1);
@@ -266,22 +561,8 @@ static int build_plan(int ndim, const double *W, int Lr_in, int Lc_in, int L, in
         rp_ptr[(size_t)t * np1 + p->npairs] = (int32_t)rp_i.size();
         // ---- inverse inputs: G[k] = A_k y[k] - i A_k y[N-k] + C_k y[N2+k] - i C_k y[N2-k]
         std::vector<std::vector<std::pair<int, cd>>> gcon(N2);
-        const cd I(0, 1);
-        auto Ak = [&](long long k) { return expi(M_PI * (double)k / (2.0 * N)) * (1.0 + I * tw(-k, N)); };
-        auto Ck = [&](long long k) { return expi(M_PI * (double)(k + N2) / (2.0 * N)) * (1.0 - I * tw(-k, N)); };
-        const double gsc = sc / sqrt2;  // sqrt(2 W/L) * (1/2)
-        for (int i = 0; i < Mr; ++i) {
-            const long long q = o0[i];
-            if (q < N2) {
-                gcon[q].push_back({i, Ak(q) * gsc});
-                gcon[N2 - q].push_back({i, -I * Ck(N2 - q) * gsc});
-            } else if (q > N2) {
-                gcon[N - q].push_back({i, -I * Ak(N - q) * gsc});
-                gcon[q - N2].push_back({i, Ck(q - N2) * gsc});
-            } else {
-                gcon[0].push_back({i, Ck(0) * (1.0 - I) * gsc});
-            }
-        }
+        for (int i = 0; i < Mr; ++i)
+            inv_contrib(o0[i], N, N2, sc, [&](long long k, cd c) { gcon[k].push_back({i, c}); });
         std::vector<std::vector<int>> slots_by_pair(p->npairs);
         for (int k = 0; k < N2; ++k)
             if (!gcon[k].empty()) slots_by_pair[pair_of(k)].push_back(k);
@@ -325,6 +606,7 @@ static int build_plan(int ndim, const double *W, int Lr_in, int Lc_in, int L, in
     SG_TRY(upload_cx(pp, &pp->twHi, twHi));
     SG_TRY(upload_cx(pp, &pp->twLo, twLo));
     SG_TRY(upload(pp, &pp->dW, Wd));
+    if (pp->regular) SG_TRY(build_regular(pp, order0, order1, t_scale));
     return SG_OK;
     }();
     if (rc != SG_OK) {
@@ -336,9 +618,52 @@ static int build_plan(int ndim, const double *W, int Lr_in, int Lc_in, int L, in
 }
 
 template <typename T>
+static int decode_regular(sg_amp_plan *p, const void *d_y, int B, const int32_t *d_true, double awgn_var, int t_max,
+                          double rtol, int phi_method, int32_t *d_map, int32_t *d_tfinal, double *d_nmse,
+                          double *d_psi, hipStream_t s) {
+    SG_TRY(ensure_ws(p, B, t_max));
+    RegTables<T> tb = rtables<T>(p);
+    RegBufs<T> bf = rbufs<T>(p, B, d_y);
+    bf.true_idx = d_true;
+    AmpScalars sc;
+    sc.psi = p->ws_psi; sc.psi_prev = p->ws_psi_prev; sc.phi_prev = p->ws_phi_prev; sc.gamma = p->ws_gamma;
+    sc.bcoef = p->ws_bco; sc.nmse = p->ws_nmse; sc.t_final = p->ws_tfinal;
+    AmpParams pr;
+    pr.W = p->dW; pr.awgn_var = awgn_var; pr.rtol = rtol;
+    pr.atol = 2e-15;  // 2*np.finfo(float).resolution, sparc.py:916
+    pr.phi_method = phi_method; pr.t_max = t_max;
+    SG_TRY(reg_launch_init(B, p->Lc, t_max, p->ws_nmse, p->ws_active, p->ws_tfinal, s));
+    std::vector<int32_t> act(B);
+    for (int t = 0; t < t_max - 1; ++t) {
+        if (t > 0) SG_TRY(reg_launch_ab<T>(tb, bf, s));
+        SG_TRY(reg_launch_ctrl0<T>(tb, bf, sc, pr, t, s));
+        SG_TRY(reg_launch_az<T>(tb, bf, t, s));
+        SG_TRY(reg_launch_merge<T>(tb, bf, sc, pr, t, s));
+        if (t % 4 == 3 && t + 1 < t_max - 1) {  // skip the remaining launches once every codeword stopped
+            SG_HIP(hipMemcpyAsync(act.data(), p->ws_active, sizeof(int32_t) * B, hipMemcpyDeviceToHost, s));
+            SG_HIP(hipStreamSynchronize(s));
+            bool any = false;
+            for (int b = 0; b < B; ++b) any |= act[b] != 0;
+            if (!any) break;
+        }
+    }
+    SG_HIP(hipMemsetAsync(p->ws_argmax, 0x7f, sizeof(int32_t) * B * p->L, s));
+    SG_TRY(reg_launch_map<T>(tb, bf, s));
+    if (d_map) SG_HIP(hipMemcpyAsync(d_map, p->ws_argmax, sizeof(int32_t) * B * p->L, hipMemcpyDeviceToDevice, s));
+    if (d_tfinal) SG_HIP(hipMemcpyAsync(d_tfinal, p->ws_tfinal, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
+    if (d_nmse) SG_HIP(hipMemcpyAsync(d_nmse, p->ws_nmse, sizeof(double) * B * t_max * p->Lc, hipMemcpyDeviceToDevice, s));
+    if (d_psi) SG_HIP(hipMemcpyAsync(d_psi, p->ws_psi, sizeof(double) * B * p->Lc, hipMemcpyDeviceToDevice, s));
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
+template <typename T>
 static int decode_impl(sg_amp_plan *p, const void *d_y, int B, const int32_t *d_true, double awgn_var, int t_max,
                        double rtol, int phi_method, int32_t *d_map, int32_t *d_tfinal, double *d_nmse, double *d_psi,
                        hipStream_t s) {
+    if (p->regular)
+        return decode_regular<T>(p, d_y, B, d_true, awgn_var, t_max, rtol, phi_method, d_map, d_tfinal, d_nmse,
+                                 d_psi, s);
     SG_TRY(ensure_ws(p, B, t_max));
     AmpTables<T> tb = tables<T>(p);
     AmpBufs<T> bf = bufs<T>(p, B, d_y);
@@ -380,6 +705,27 @@ template <typename T>
 static int apply_impl(sg_amp_plan *p, int transpose, const void *d_in, int in_is_double, int B, void *d_out,
                       int out_double, hipStream_t s) {
     SG_TRY(ensure_ws(p, B, 2));
+    if (p->regular) {
+        RegTables<T> rt = rtables<T>(p);
+        RegBufs<T> rf = rbufs<T>(p, B, nullptr);
+        rf.mode = 1;
+        if (!transpose) {
+            SG_TRY(amp_launch_cast<T>(d_in, in_is_double, (T *)p->ws_s, (size_t)B * p->LM, s));
+            rf.ext_in = (const T *)p->ws_s;
+            rf.ext_out = out_double ? (T *)p->ws_z : (T *)d_out;
+            SG_TRY(reg_launch_ab<T>(rt, rf, s));
+            SG_TRY(reg_launch_ab_finish<T>(rt, rf, s));
+            if (out_double) SG_TRY(amp_launch_uncast<T>((T *)p->ws_z, (double *)d_out, (size_t)B * p->n, s));
+        } else {
+            SG_TRY(amp_launch_cast<T>(d_in, in_is_double, (T *)p->ws_y, (size_t)B * p->n, s));
+            rf.ext_in = (const T *)p->ws_y;
+            rf.ext_out = out_double ? (T *)p->ws_s : (T *)d_out;
+            SG_TRY(reg_launch_az<T>(rt, rf, 0, s));
+            if (out_double) SG_TRY(amp_launch_uncast<T>((T *)p->ws_s, (double *)d_out, (size_t)B * p->LM, s));
+        }
+        SG_HIP(hipStreamSynchronize(s));
+        return SG_OK;
+    }
     AmpTables<T> tb = tables<T>(p);
     AmpBufs<T> bf = bufs<T>(p, B, nullptr);
     // all codewords active
@@ -439,8 +785,8 @@ int sg_amp_plan_info(const sg_amp_plan *p, int *w, int *nT, int *Mr, int *Mc, in
     if (nT) *nT = p->nT;
     if (Mr) *Mr = p->Mr;
     if (Mc) *Mc = p->Mc;
-    if (P) *P = p->P;
-    if (Q) *Q = p->Q;
+    if (P) *P = p->regular ? p->rP : p->P;
+    if (Q) *Q = p->regular ? p->rQ : p->Q;
     return SG_OK;
 }
 

@@ -152,4 +152,83 @@ __device__ void lds_fft(cx<T> *d, int log2n, int nseq, int es, int ss, const cx<
     }
 }
 
+// ---------------------------------------------------------------------------
+// Single-sequence variant for the LDS-resident stage-1 transforms of the
+// regular AMP engine: one sequence of n = 2^log2n points in d[0..n), every
+// index computed with shifts and masks (no integer division), the twiddles of
+// a butterfly loaded before its first use.
+// Twiddles come from a per-stage table laid out in thread order:
+// stw[k * (R - 1) + r - 1] = w_{Ns R}^{r k} (forward), so the R - 1 twiddles of
+// a butterfly are contiguous and a wavefront reads a contiguous range.
+template <typename T, bool INV, int R, int EPT>
+__device__ __forceinline__ void stockham1_stage(cx<T> *d, int log2n, int log2Ns, const cx<T> *__restrict__ stw,
+                                                int tid, int nthr) {
+    constexpr int NB = EPT / R;
+    constexpr int LR = (R == 2) ? 1 : (R == 4) ? 2 : (R == 8) ? 3 : 4;
+    const int nbf = 1 << (log2n - LR);
+    const int Ns = 1 << log2Ns;
+    cx<T> v[EPT];
+    int base_out[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        const int j = tid + i * nthr;
+        const int k = j & (Ns - 1);
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[i * R + r] = d[j + r * nbf];
+        if (log2Ns > 0) {
+            cx<T> w[R];
+#pragma unroll
+            for (int r = 1; r < R; ++r) w[r] = stw[k * (R - 1) + r - 1];
+#pragma unroll
+            for (int r = 1; r < R; ++r) {
+                if (INV) w[r].y = -w[r].y;
+                v[i * R + r] = cmul(v[i * R + r], w[r]);
+            }
+        }
+        dftR<T, INV, R>(&v[i * R]);
+        base_out[i] = ((j - k) << LR) + k;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) d[base_out[i] + r * Ns] = v[i * R + r];
+    }
+    __syncthreads();
+}
+
+// n = 2^log2n, nthr * EPT == n; radix-8 stages with one radix-4 or two
+// radix-4 (or one radix-2) for the remainder, smallest radices first.
+// Radix plan shared with the host table builder (fft_stage_plan).
+__host__ __device__ inline void fft1_plan(int log2n, int *n2, int *n4, int *n8) {
+    int a8 = log2n / 3, rem = log2n % 3, c4 = 0, c2 = 0;
+    if (rem == 2) c4 = 1;
+    else if (rem == 1) {
+        if (a8 >= 1) { a8 -= 1; c4 = 2; }
+        else c2 = 1;
+    }
+    *n2 = c2; *n4 = c4; *n8 = a8;
+}
+
+// stw: concatenated per-stage tables (stage order), see stockham1_stage.
+template <typename T, bool INV, int EPT>
+__device__ void lds_fft1(cx<T> *d, int log2n, const cx<T> *__restrict__ stw, int tid, int nthr) {
+    int n2, n4, n8;
+    fft1_plan(log2n, &n2, &n4, &n8);
+    int lns = 0;
+    size_t off = 0;
+    for (int s = 0; s < n2; ++s) {
+        stockham1_stage<T, INV, 2, EPT>(d, log2n, lns, stw + off, tid, nthr);
+        off += (size_t)(1 << lns) * 1; lns += 1;
+    }
+    for (int s = 0; s < n4; ++s) {
+        stockham1_stage<T, INV, 4, EPT>(d, log2n, lns, stw + off, tid, nthr);
+        off += (size_t)(1 << lns) * 3; lns += 2;
+    }
+    for (int s = 0; s < n8; ++s) {
+        stockham1_stage<T, INV, 8, EPT>(d, log2n, lns, stw + off, tid, nthr);
+        off += (size_t)(1 << lns) * 7; lns += 3;
+    }
+}
+
 }  // namespace sg
