@@ -99,6 +99,7 @@ struct RegTables {
     const cx<T> *stw;         // per-stage P-point FFT twiddles (lds_fft1)
     const cx<T> *twa, *twb;   // w_N2^(m2 k1) = twa[m2][k1 & 63] * twb[m2][k1 >> 6]
     int nB;                   // ceil(P / 64)
+    int skip;                 // timing ablation only (SG_AMP_SKIP): 1 FFT, 2 gather/scatter, 4 row I/O
 };
 
 template <typename T>
@@ -135,6 +136,7 @@ int reg_launch_map(const RegTables<T> &tb, const RegBufs<T> &bf, hipStream_t s);
 template <typename T>
 int reg_launch_ab_finish(const RegTables<T> &tb, const RegBufs<T> &bf, hipStream_t s);
 size_t reg_stage1_lds(int P, int Lblk, size_t real_bytes);
+inline int reg_ept(int P) { return P / 1024 > 8 ? P / 1024 : 8; }  // stage-1 elements per thread
 int reg_launch_init(int B, int Lc, int t_max, double *nmse, int32_t *active, int32_t *t_final, hipStream_t s);
 
 template <typename T>

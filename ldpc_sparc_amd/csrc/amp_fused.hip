@@ -63,21 +63,22 @@ __device__ __forceinline__ double reg_block_sum(double v, double *red) {
 constexpr int REG_CH = 8;  // entries a thread loads before using them
 
 size_t reg_stage1_lds(int P, int Lblk, size_t real_bytes) {
-    return (size_t)P * 2 * real_bytes + (size_t)2 * Lblk * real_bytes;
+    return (size_t)(P + (P >> 4)) * 2 * real_bytes + (size_t)2 * Lblk * real_bytes;
 }
 
 // ------------------------------------------------------------------ ab stage 1
-template <typename T, int EPT>
+template <typename T, int EPT, int LOG2P>
 __global__ __launch_bounds__(1024) void reg_ab_stage1(RegTables<T> tb, RegBufs<T> bf) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     cx<T> *d = reinterpret_cast<cx<T> *>(smem);
     T *dr = reinterpret_cast<T *>(smem);
-    T *sM = dr + 2 * (size_t)tb.P;
+    const int Pp = tb.P + (tb.P >> 4);  // padded FFT array (fpad)
+    T *sM = dr + 2 * (size_t)Pp;
     T *sI = sM + tb.Lblk;
     const int m2 = blockIdx.x, t = blockIdx.y, cw = blockIdx.z;
-    if (bf.mode == 0 && !bf.active[cw]) return;
+    if (bf.mode == 0 && !bf.active[cw] && !tb.skip) return;
     const int tid = threadIdx.x, nthr = blockDim.x;
-    for (int i = tid; i < 2 * tb.P; i += nthr) dr[i] = T(0);
+    for (int i = tid; i < 2 * Pp; i += nthr) dr[i] = T(0);
     const size_t tc = (size_t)t * tb.Mc;
     T tau = T(1), inv_tau = T(1);
     if (bf.mode == 0) {
@@ -94,7 +95,7 @@ __global__ __launch_bounds__(1024) void reg_ab_stage1(RegTables<T> tb, RegBufs<T
     const int32_t *cp = tb.cls_ptr + (size_t)t * (tb.Q + 1);
     const int q0 = cp[m2], q1 = cp[m2 + 1];
     const uint16_t *loc = tb.cls_loc + tc;
-    if (bf.mode == 0) {
+    if (bf.mode == 0 && !(tb.skip & 2)) {
         const T *s = bf.s + (size_t)cw * tb.LM + tc;
         const uint16_t *sec = tb.cls_sec + tc;
         for (int base = q0 + tid; base < q1; base += REG_CH * nthr) {
@@ -114,14 +115,17 @@ __global__ __launch_bounds__(1024) void reg_ab_stage1(RegTables<T> tb, RegBufs<T
                 if (base + i * nthr < q1)
                     dr[lc[i]] = rexp<T>(sm_arg<T>(v[i], sM[sc[i]], tau, inv_tau)) * sI[sc[i]];
         }
-    } else {
+    } else if (bf.mode != 0) {
         const T *x = bf.ext_in + (size_t)cw * tb.LM + tc;
         const int32_t *cj = tb.cls_j + tc;
         for (int q = q0 + tid; q < q1; q += nthr) dr[loc[q]] = x[cj[q]];
     }
     __syncthreads();
-    lds_fft1<T, false, EPT>(d, tb.log2P, tb.stw, tid, nthr);
-    const int nR = tb.nR[t];
+    if (!(tb.skip & 1)) {
+        if constexpr (LOG2P > 0) lds_fft1_ct<T, false, EPT, LOG2P>(d, tb.stw, tid);
+        else lds_fft1<T, false, EPT>(d, tb.log2P, tb.stw, tid, nthr);
+    }
+    const int nR = (tb.skip & 4) ? 0 : tb.nR[t];
     const int32_t *rk = tb.row_k1 + (size_t)t * tb.nRmax;
     cx<T> *out = bf.tu + (((size_t)cw * tb.nT + t) * tb.Q + m2) * tb.nRmax;
     for (int base = tid; base < nR; base += REG_CH * nthr) {
@@ -137,7 +141,7 @@ __global__ __launch_bounds__(1024) void reg_ab_stage1(RegTables<T> tb, RegBufs<T
 #pragma unroll
         for (int i = 0; i < REG_CH; ++i) {
             const int r = base + i * nthr;
-            if (r < nR) out[r] = cmul(d[k1[i]], w[i]);
+            if (r < nR) out[r] = cmul(d[fpad(k1[i])], w[i]);
         }
     }
 }
@@ -149,7 +153,7 @@ __global__ __launch_bounds__(256) void reg_ab_stage2(RegTables<T> tb, RegBufs<T>
     cx<T> *d = reinterpret_cast<cx<T> *>(smem);  // [Q][RB]
     cx<T> *twq = d + (size_t)tb.Q * tb.RB;       // [Q]
     const int rb = blockIdx.x, t = blockIdx.y, cw = blockIdx.z;
-    if (bf.mode == 0 && !bf.active[cw]) return;
+    if (bf.mode == 0 && !bf.active[cw] && !tb.skip) return;
     const int nR = tb.nR[t];
     const int r0 = rb * tb.RB;
     if (r0 >= nR) return;
@@ -157,9 +161,25 @@ __global__ __launch_bounds__(256) void reg_ab_stage2(RegTables<T> tb, RegBufs<T>
     const int tid = threadIdx.x, nthr = blockDim.x;
     for (int i = tid; i < tb.Q; i += nthr) twq[i] = tb.twQ[i];
     const cx<T> *src = bf.tu + ((size_t)cw * tb.nT + t) * tb.Q * tb.nRmax;
-    for (int e = tid; e < tb.Q * nr; e += nthr) {
-        const int m2 = e / nr, r = e - m2 * nr;
-        d[m2 * tb.RB + r] = src[(size_t)m2 * tb.nRmax + r0 + r];
+    // rows [r0, r1) of every m2 plane; REG_CH loads in flight per thread
+    for (int base = tid; base < tb.Q * nr; base += REG_CH * nthr) {
+        cx<T> v[REG_CH];
+#pragma unroll
+        for (int i = 0; i < REG_CH; ++i) {
+            const int e = base + i * nthr;
+            if (e < tb.Q * nr) {
+                const int m2 = e / nr, r = e - m2 * nr;
+                v[i] = src[(size_t)m2 * tb.nRmax + r0 + r];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < REG_CH; ++i) {
+            const int e = base + i * nthr;
+            if (e < tb.Q * nr) {
+                const int m2 = e / nr, r = e - m2 * nr;
+                d[m2 * tb.RB + r] = v[i];
+            }
+        }
     }
     __syncthreads();
     const int32_t *kp = tb.kptr + (size_t)t * (tb.nRmax + 1);
@@ -206,8 +226,11 @@ __global__ __launch_bounds__(256) void reg_az_stage1(RegTables<T> tb, RegBufs<T>
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     cx<T> *twq = reinterpret_cast<cx<T> *>(smem);  // [Q]
     cx<T> *g = twq + tb.Q;                           // G of the block's needed indices
+    int *rkp = reinterpret_cast<int *>(g + tb.maxKb);  // [RB + 1] kptr - ka, [RB] k1, [maxKb] k2
+    int *rk1 = rkp + tb.RB + 1;
+    int *rk2 = rk1 + tb.RB;
     const int rb = blockIdx.x, t = blockIdx.y, cw = blockIdx.z;
-    if (bf.mode == 0 && !bf.active[cw]) return;
+    if (bf.mode == 0 && !bf.active[cw] && !tb.skip) return;
     const int nR = tb.nR[t];
     const int r0 = rb * tb.RB;
     if (r0 >= nR) return;
@@ -233,36 +256,41 @@ __global__ __launch_bounds__(256) void reg_az_stage1(RegTables<T> tb, RegBufs<T>
             }
         }
         g[k - ka] = acc;
+        rk2[k - ka] = tb.kk2[(size_t)t * tb.nKmax + k];
+    }
+    for (int r = tid; r <= nr; r += nthr) {
+        rkp[r] = kp[r0 + r] - ka;
+        if (r < nr) rk1[r] = tb.row_k1[(size_t)t * tb.nRmax + r0 + r];
     }
     __syncthreads();
-    const int32_t *k2s = tb.kk2 + (size_t)t * tb.nKmax, *rk = tb.row_k1 + (size_t)t * tb.nRmax;
     cx<T> *dst = bf.tu + ((size_t)cw * tb.nT + t) * tb.Q * tb.nRmax;
     const int qm = tb.Q - 1;
     for (int e = tid; e < tb.Q * nr; e += nthr) {
-        const int m2 = e / nr, r = e - m2 * nr, rho = r0 + r;
-        const int a = kp[rho], b = kp[rho + 1];
+        const int m2 = e / nr, r = e - m2 * nr;
+        const int a = rkp[r], b = rkp[r + 1];
         cx<T> acc{T(0), T(0)};
         for (int k = a; k < b; ++k) {
-            const cx<T> v = g[k - ka], w = twq[(m2 * k2s[k]) & qm];  // v * conj(w)
+            const cx<T> v = g[k], w = twq[(m2 * rk2[k]) & qm];  // v * conj(w)
             acc.x += v.x * w.x + v.y * w.y;
             acc.y += v.y * w.x - v.x * w.y;
         }
-        dst[(size_t)m2 * tb.nRmax + rho] = cmul(acc, cconj(reg_tw2(tb, m2, rk[rho])));
+        dst[(size_t)m2 * tb.nRmax + r0 + r] = cmul(acc, cconj(reg_tw2(tb, m2, rk1[r])));
     }
 }
 
 // ------------------------------------------------------------------ az stage 2
-template <typename T, int EPT>
+template <typename T, int EPT, int LOG2P>
 __global__ __launch_bounds__(1024) void reg_az_stage2(RegTables<T> tb, RegBufs<T> bf, int t_iter) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     cx<T> *d = reinterpret_cast<cx<T> *>(smem);
     T *dr = reinterpret_cast<T *>(smem);
-    T *sM = dr + 2 * (size_t)tb.P;
+    const int Pp = tb.P + (tb.P >> 4);  // padded FFT array (fpad)
+    T *sM = dr + 2 * (size_t)Pp;
     T *sI = sM + tb.Lblk;
     const int m2 = blockIdx.x, t = blockIdx.y, cw = blockIdx.z;
-    if (bf.mode == 0 && !bf.active[cw]) return;
+    if (bf.mode == 0 && !bf.active[cw] && !tb.skip) return;
     const int tid = threadIdx.x, nthr = blockDim.x;
-    for (int i = tid; i < 2 * tb.P; i += nthr) dr[i] = T(0);
+    for (int i = tid; i < 2 * Pp; i += nthr) dr[i] = T(0);
     T tp = T(1), inv_tp = T(1);
     const bool have_beta = bf.mode == 0 && t_iter > 0;
     if (have_beta) {  // beta of the previous iteration = softmax(s_prev) with tau_prev
@@ -276,7 +304,7 @@ __global__ __launch_bounds__(1024) void reg_az_stage2(RegTables<T> tb, RegBufs<T
         inv_tp = (T)(1.0 / tv);
     }
     __syncthreads();
-    const int nR = tb.nR[t];
+    const int nR = (tb.skip & 4) ? 0 : tb.nR[t];
     const int32_t *rk = tb.row_k1 + (size_t)t * tb.nRmax;
     const cx<T> *src = bf.tu + (((size_t)cw * tb.nT + t) * tb.Q + m2) * tb.nRmax;
     for (int base = tid; base < nR; base += REG_CH * nthr) {
@@ -292,10 +320,13 @@ __global__ __launch_bounds__(1024) void reg_az_stage2(RegTables<T> tb, RegBufs<T
         }
 #pragma unroll
         for (int i = 0; i < REG_CH; ++i)
-            if (base + i * nthr < nR) d[k1[i]] = v[i];
+            if (base + i * nthr < nR) d[fpad(k1[i])] = v[i];
     }
     __syncthreads();
-    lds_fft1<T, true, EPT>(d, tb.log2P, tb.stw, tid, nthr);
+    if (!(tb.skip & 1)) {
+        if constexpr (LOG2P > 0) lds_fft1_ct<T, true, EPT, LOG2P>(d, tb.stw, tid);
+        else lds_fft1<T, true, EPT>(d, tb.log2P, tb.stw, tid, nthr);
+    }
     const size_t tc = (size_t)t * tb.Mc;
     const int32_t *cp = tb.cls_ptr + (size_t)t * (tb.Q + 1);
     const int q0 = cp[m2], q1 = cp[m2 + 1];
@@ -313,6 +344,7 @@ __global__ __launch_bounds__(1024) void reg_az_stage2(RegTables<T> tb, RegBufs<T
     // s = beta + tau * Az(z/phi) for the thread's entries (a class holds at
     // most 2P = 2 EPT nthr entries); kept in registers until every u is read
     T snv[2 * EPT];
+    const int qe = (tb.skip & 2) ? q0 : q1;
 #pragma unroll
     for (int c = 0; c < 2 * EPT; c += REG_CH) {
         T v[REG_CH];
@@ -320,7 +352,7 @@ __global__ __launch_bounds__(1024) void reg_az_stage2(RegTables<T> tb, RegBufs<T
 #pragma unroll
         for (int i = 0; i < REG_CH; ++i) {
             const int q = q0 + tid + (c + i) * nthr;
-            if (q < q1) {
+            if (q < qe) {
                 lc[i] = loc[q];
                 if (have_beta) {
                     v[i] = s[q];
@@ -331,7 +363,7 @@ __global__ __launch_bounds__(1024) void reg_az_stage2(RegTables<T> tb, RegBufs<T
 #pragma unroll
         for (int i = 0; i < REG_CH; ++i) {
             const int q = q0 + tid + (c + i) * nthr;
-            if (q < q1) {
+            if (q < qe) {
                 T b = T(0);
                 if (have_beta) b = rexp<T>(sm_arg<T>(v[i], sM[sc[i]], tp, inv_tp)) * sI[sc[i]];
                 const T sn = b + tau * dr[lc[i]];
@@ -342,21 +374,23 @@ __global__ __launch_bounds__(1024) void reg_az_stage2(RegTables<T> tb, RegBufs<T
     }
     __syncthreads();
 #pragma unroll
-    for (int c = 0; c < 2 * EPT; ++c) {  // s of the class, contiguous in LDS (class order)
+    for (int c = 0; c < 2 * EPT; ++c) {  // s of the class in class order, skewed by fpad
         const int q = q0 + tid + c * nthr;
-        if (q < q1) dr[q - q0] = snv[c];
+        if (q < qe) dr[fpad(q - q0)] = snv[c];
     }
     __syncthreads();
     // per (class, section) statistics of the softmax, deterministic order
     const uint16_t *sg = tb.seg + ((size_t)t * tb.Q + m2) * (tb.Lblk + 1);
     T *pm = bf.part + (((size_t)cw * tb.nT + t) * tb.Q + m2) * 3 * (size_t)tb.Lblk;
+    // one thread per section over its contiguous segment (segments average
+    // ~16 entries: the fpad skew spreads the threads over the LDS banks)
     for (int l = tid; l < tb.Lblk; l += nthr) {
         const int a = sg[l], b = sg[l + 1];
         T m = -INFINITY;
-        for (int q = a; q < b; ++q) m = fmax(m, dr[q]);
+        for (int q = a; q < b; ++q) m = fmax(m, dr[fpad(q)]);
         T S1 = T(0), S2 = T(0);
         for (int q = a; q < b; ++q) {
-            const T e = rexp<T>(sm_arg<T>(dr[q], m, tau, inv_tau));
+            const T e = rexp<T>(sm_arg<T>(dr[fpad(q)], m, tau, inv_tau));
             S1 += e;
             S2 += e * e;
         }
@@ -535,21 +569,17 @@ int reg_launch_init(int B, int Lc, int t_max, double *nmse, int32_t *active, int
 }
 
 // ------------------------------------------------------------------ launchers
-template <typename T>
-static int reg_ept(int P) {
-    const int e = P / 1024;
-    return e > 8 ? e : 8;
-}
-
-template <typename T, int EPT>
+template <typename T, int EPT, int LOG2P>
 static void launch_s1(const RegTables<T> &tb, const RegBufs<T> &bf, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL((reg_ab_stage1<T, EPT>), dim3(tb.Q, tb.nT, bf.B), dim3(tb.P / EPT), lds, s, tb, bf);
+    hipLaunchKernelGGL((reg_ab_stage1<T, EPT, LOG2P>), dim3(tb.Q, tb.nT, bf.B), dim3(tb.P / EPT), lds, s, tb, bf);
 }
-template <typename T, int EPT>
+template <typename T, int EPT, int LOG2P>
 static void launch_s2i(const RegTables<T> &tb, const RegBufs<T> &bf, int t_iter, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL((reg_az_stage2<T, EPT>), dim3(tb.Q, tb.nT, bf.B), dim3(tb.P / EPT), lds, s, tb, bf,
+    hipLaunchKernelGGL((reg_az_stage2<T, EPT, LOG2P>), dim3(tb.Q, tb.nT, bf.B), dim3(tb.P / EPT), lds, s, tb, bf,
                        t_iter);
 }
+// compile-time FFT for the benchmark sizes (f32: P = 2^14; f64: P = 2^13)
+constexpr int reg_hot_log2p(bool dbl) { return dbl ? 13 : 14; }
 
 template <typename T>
 static int reg_set_attrs() {
@@ -557,8 +587,10 @@ static int reg_set_attrs() {
     if (done) return SG_OK;
     const int mx = 160 * 1024;
 #define SG_LDS_ATTR(K) SG_HIP(hipFuncSetAttribute((const void *)(K), hipFuncAttributeMaxDynamicSharedMemorySize, mx))
-    SG_LDS_ATTR((reg_ab_stage1<T, 8>)); SG_LDS_ATTR((reg_ab_stage1<T, 16>));
-    SG_LDS_ATTR((reg_az_stage2<T, 8>)); SG_LDS_ATTR((reg_az_stage2<T, 16>));
+    constexpr int H = reg_hot_log2p(sizeof(T) == 8), HE = sizeof(T) == 8 ? 8 : 16;
+    SG_LDS_ATTR((reg_ab_stage1<T, 8, 0>)); SG_LDS_ATTR((reg_ab_stage1<T, 16, 0>));
+    SG_LDS_ATTR((reg_az_stage2<T, 8, 0>)); SG_LDS_ATTR((reg_az_stage2<T, 16, 0>));
+    SG_LDS_ATTR((reg_ab_stage1<T, HE, H>)); SG_LDS_ATTR((reg_az_stage2<T, HE, H>));
     SG_LDS_ATTR((reg_ab_stage2<T>)); SG_LDS_ATTR((reg_az_stage1<T>));
 #undef SG_LDS_ATTR
     done = true;
@@ -570,11 +602,13 @@ int reg_launch_ab(const RegTables<T> &tb, const RegBufs<T> &bf, hipStream_t s) {
     if (bf.B <= 0) return SG_OK;
     SG_TRY(reg_set_attrs<T>());
     const size_t lds1 = reg_stage1_lds(tb.P, tb.Lblk, sizeof(T));
-    const int ept = reg_ept<T>(tb.P);
+    const int ept = reg_ept(tb.P);
     {
         ProfScope ps(SG_PH_AB_A, s);
-        if (ept == 8) launch_s1<T, 8>(tb, bf, lds1, s);
-        else if (ept == 16) launch_s1<T, 16>(tb, bf, lds1, s);
+        constexpr int H = reg_hot_log2p(sizeof(T) == 8), HE = sizeof(T) == 8 ? 8 : 16;
+        if (tb.log2P == H && ept == HE) launch_s1<T, HE, H>(tb, bf, lds1, s);
+        else if (ept == 8) launch_s1<T, 8, 0>(tb, bf, lds1, s);
+        else if (ept == 16) launch_s1<T, 16, 0>(tb, bf, lds1, s);
         else return fail(SG_ERR_UNSUPPORTED, "stage-1 FFT length P=%d unsupported", tb.P);
     }
     SG_HIP(hipGetLastError());
@@ -601,16 +635,18 @@ int reg_launch_az(const RegTables<T> &tb, const RegBufs<T> &bf, int t_iter, hipS
     SG_TRY(reg_set_attrs<T>());
     {
         ProfScope ps(SG_PH_AZ_A, s);
-        const size_t ldsg = sizeof(cx<T>) * ((size_t)(tb.maxKb > 0 ? tb.maxKb : 1) + tb.Q);
+        const size_t ldsg = sizeof(cx<T>) * ((size_t)tb.maxKb + tb.Q) + sizeof(int) * (2 * (size_t)tb.RB + 1 + tb.maxKb);
         hipLaunchKernelGGL((reg_az_stage1<T>), dim3(tb.nrb, tb.nT, bf.B), dim3(256), ldsg, s, tb, bf);
     }
     SG_HIP(hipGetLastError());
     const size_t lds1 = reg_stage1_lds(tb.P, tb.Lblk, sizeof(T));
-    const int ept = reg_ept<T>(tb.P);
+    const int ept = reg_ept(tb.P);
     {
         ProfScope ps(SG_PH_AZ_B, s);
-        if (ept == 8) launch_s2i<T, 8>(tb, bf, t_iter, lds1, s);
-        else if (ept == 16) launch_s2i<T, 16>(tb, bf, t_iter, lds1, s);
+        constexpr int H = reg_hot_log2p(sizeof(T) == 8), HE = sizeof(T) == 8 ? 8 : 16;
+        if (tb.log2P == H && ept == HE) launch_s2i<T, HE, H>(tb, bf, t_iter, lds1, s);
+        else if (ept == 8) launch_s2i<T, 8, 0>(tb, bf, t_iter, lds1, s);
+        else if (ept == 16) launch_s2i<T, 16, 0>(tb, bf, t_iter, lds1, s);
         else return fail(SG_ERR_UNSUPPORTED, "stage-1 FFT length P=%d unsupported", tb.P);
     }
     SG_HIP(hipGetLastError());

@@ -234,7 +234,7 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
     const int Q = (int)(N2 / P);
     p->rP = P; p->rQ = Q; p->rlog2P = ilog2(P); p->Lblk = Lblk;
     const size_t cxb = 2 * rb;
-    p->RB = (int)std::min<size_t>(256, std::max<size_t>(1, 65536 / ((size_t)Q * cxb)));
+    p->RB = (int)std::min<size_t>(128, std::max<size_t>(1, 32768 / ((size_t)Q * cxb)));
 
     std::vector<std::vector<int32_t>> row_k1(nT), kptr(nT), kk2(nT), krho(nT), oa(nT), ob(nT), gi(nT);
     std::vector<std::vector<cd>> oc(nT), gc(nT);
@@ -255,7 +255,7 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
             used[sl] = 1;
             const long long m = sl >> 1;
             m2of[j] = (int)(m % Q);
-            locof[j] = (int)(2 * (m / Q) + (sl & 1));
+            locof[j] = (int)(2 * fpad((int)(m / Q)) + (sl & 1));  // padded LDS layout of lds_fft1
             cnt[m2of[j] + 1]++;
         }
         int32_t *cpt = cls_ptr.data() + (size_t)t * (Q + 1);
@@ -374,18 +374,16 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
     // per-stage twiddles of the P-point FFT in thread order (fft.hpp lds_fft1)
     std::vector<cd> stw;
     {
-        int n2, n4, n8;
-        fft1_plan(p->rlog2P, &n2, &n4, &n8);
+        int radix[8];
+        const int ns = fft1_plan(p->rlog2P, reg_ept(P), radix);
         int lns = 0;
-        auto stage = [&](int R, int LR) {
+        for (int st = 0; st < ns; ++st) {
+            const int R = radix[st];
             const long long Ns = 1LL << lns;
             for (long long k = 0; k < Ns; ++k)
                 for (int r = 1; r < R; ++r) stw.push_back(tw(r * k, Ns * R));
-            lns += LR;
-        };
-        for (int i = 0; i < n2; ++i) stage(2, 1);
-        for (int i = 0; i < n4; ++i) stage(4, 2);
-        for (int i = 0; i < n8; ++i) stage(8, 3);
+            lns += ilog2(R);
+        }
         if (stw.empty()) stw.push_back(cd(1, 0));
     }
     const int nB = (P + 63) / 64;
@@ -433,6 +431,8 @@ static RegTables<T> rtables(const sg_amp_plan *p) {
     tb.twHi = (const cx<T> *)p->twHi; tb.twLo = (const cx<T> *)p->twLo;
     tb.stw = (const cx<T> *)p->r_stw; tb.twa = (const cx<T> *)p->r_twa; tb.twb = (const cx<T> *)p->r_twb;
     tb.nB = p->nB;
+    const char *sk = std::getenv("SG_AMP_SKIP");  // timing ablation only: results are wrong when set
+    tb.skip = sk ? std::atoi(sk) : 0;
     return tb;
 }
 
@@ -639,7 +639,7 @@ static int decode_regular(sg_amp_plan *p, const void *d_y, int B, const int32_t 
         SG_TRY(reg_launch_ctrl0<T>(tb, bf, sc, pr, t, s));
         SG_TRY(reg_launch_az<T>(tb, bf, t, s));
         SG_TRY(reg_launch_merge<T>(tb, bf, sc, pr, t, s));
-        if (t % 4 == 3 && t + 1 < t_max - 1) {  // skip the remaining launches once every codeword stopped
+        if (t % 4 == 3 && t + 1 < t_max - 1 && !tb.skip) {  // skip the remaining launches once every codeword stopped
             SG_HIP(hipMemcpyAsync(act.data(), p->ws_active, sizeof(int32_t) * B, hipMemcpyDeviceToHost, s));
             SG_HIP(hipStreamSynchronize(s));
             bool any = false;

@@ -76,11 +76,48 @@ __device__ __forceinline__ void dft8(cx<T> *a) {
     }
 }
 
+// 16-point DFT as 4 x 4: inputs n = 4 n1 + n2, outputs k = k1 + 4 k2.
+template <typename T, bool INV>
+__device__ __forceinline__ void dft16(cx<T> *a) {
+    const T c1 = T(0.92387953251128675612818318939678828682);  // cos(pi/8)
+    const T s1 = T(0.38268343236508977172845998403039886676);  // sin(pi/8)
+    const T r2 = T(0.70710678118654752440084436210484903928);
+    cx<T> y[4][4];
+#pragma unroll
+    for (int n2 = 0; n2 < 4; ++n2) {
+        cx<T> v[4] = {a[n2], a[n2 + 4], a[n2 + 8], a[n2 + 12]};
+        dft4<T, INV>(v);
+#pragma unroll
+        for (int k1 = 0; k1 < 4; ++k1) y[n2][k1] = v[k1];
+    }
+    // y[n2][k1] *= w16^(n2 k1) (forward w16 = e^{-i pi/8}; inverse conjugated)
+    auto tw16 = [&](cx<T> x, T c, T s) -> cx<T> {  // x * (c - i s) forward, (c + i s) inverse
+        return INV ? cx<T>{x.x * c - x.y * s, x.x * s + x.y * c} : cx<T>{x.x * c + x.y * s, x.y * c - x.x * s};
+    };
+    y[1][1] = tw16(y[1][1], c1, s1);
+    y[1][2] = tw16(y[1][2], r2, r2);
+    y[1][3] = tw16(y[1][3], s1, c1);
+    y[2][1] = tw16(y[2][1], r2, r2);
+    y[2][2] = mul_mi<T, INV>(y[2][2]);
+    y[2][3] = tw16(y[2][3], -r2, r2);
+    y[3][1] = tw16(y[3][1], s1, c1);
+    y[3][2] = tw16(y[3][2], -r2, r2);
+    y[3][3] = tw16(y[3][3], -c1, -s1);
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) {
+        cx<T> v[4] = {y[0][k1], y[1][k1], y[2][k1], y[3][k1]};
+        dft4<T, INV>(v);
+#pragma unroll
+        for (int k2 = 0; k2 < 4; ++k2) a[k1 + 4 * k2] = v[k2];
+    }
+}
+
 template <typename T, bool INV, int R>
 __device__ __forceinline__ void dftR(cx<T> *a) {
     if (R == 2) dft2<T, INV>(a);
     else if (R == 4) dft4<T, INV>(a);
-    else dft8<T, INV>(a);
+    else if (R == 8) dft8<T, INV>(a);
+    else dft16<T, INV>(a);
 }
 
 // Sequence layout in LDS: element e of sequence s lives at d[s*ss + e*es].
@@ -160,6 +197,10 @@ __device__ void lds_fft(cx<T> *d, int log2n, int nseq, int es, int ss, const cx<
 // Twiddles come from a per-stage table laid out in thread order:
 // stw[k * (R - 1) + r - 1] = w_{Ns R}^{r k} (forward), so the R - 1 twiddles of
 // a butterfly are contiguous and a wavefront reads a contiguous range.
+// LDS layout of the single-sequence FFT: element i at fpad(i) = i + i/16,
+// which makes the power-of-two strides of the Stockham stores conflict-free.
+__host__ __device__ __forceinline__ int fpad(int i) { return i + (i >> 4); }
+
 template <typename T, bool INV, int R, int EPT>
 __device__ __forceinline__ void stockham1_stage(cx<T> *d, int log2n, int log2Ns, const cx<T> *__restrict__ stw,
                                                 int tid, int nthr) {
@@ -174,7 +215,7 @@ __device__ __forceinline__ void stockham1_stage(cx<T> *d, int log2n, int log2Ns,
         const int j = tid + i * nthr;
         const int k = j & (Ns - 1);
 #pragma unroll
-        for (int r = 0; r < R; ++r) v[i * R + r] = d[j + r * nbf];
+        for (int r = 0; r < R; ++r) v[i * R + r] = d[fpad(j + r * nbf)];
         if (log2Ns > 0) {
             cx<T> w[R];
 #pragma unroll
@@ -192,43 +233,135 @@ __device__ __forceinline__ void stockham1_stage(cx<T> *d, int log2n, int log2Ns,
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) d[base_out[i] + r * Ns] = v[i * R + r];
+        for (int r = 0; r < R; ++r) d[fpad(base_out[i] + r * Ns)] = v[i * R + r];
     }
     __syncthreads();
 }
 
 // n = 2^log2n, nthr * EPT == n; radix-8 stages with one radix-4 or two
 // radix-4 (or one radix-2) for the remainder, smallest radices first.
-// Radix plan shared with the host table builder (fft_stage_plan).
-__host__ __device__ inline void fft1_plan(int log2n, int *n2, int *n4, int *n8) {
-    int a8 = log2n / 3, rem = log2n % 3, c4 = 0, c2 = 0;
-    if (rem == 2) c4 = 1;
-    else if (rem == 1) {
-        if (a8 >= 1) { a8 -= 1; c4 = 2; }
-        else c2 = 1;
+// Radix plan shared with the host table builder: EPT 16 -> radix-16 stages
+// after one smaller first stage for the remainder; EPT 8 -> radix-8 stages
+// with radix-4 (or one radix-2) first.  Returns the number of stages.
+__host__ __device__ inline int fft1_plan(int log2n, int ept, int *radix /* [8] */) {
+    int ns = 0;
+    if (ept >= 16) {
+        const int rem = log2n % 4;
+        if (rem) radix[ns++] = 1 << rem;
+        for (int i = 0; i < log2n / 4; ++i) radix[ns++] = 16;
+    } else {
+        int a8 = log2n / 3, rem = log2n % 3;
+        if (rem == 2) radix[ns++] = 4;
+        else if (rem == 1) {
+            if (a8 >= 1) { a8 -= 1; radix[ns++] = 4; radix[ns++] = 4; }
+            else radix[ns++] = 2;
+        }
+        for (int i = 0; i < a8; ++i) radix[ns++] = 8;
     }
-    *n2 = c2; *n4 = c4; *n8 = a8;
+    return ns;
 }
 
-// stw: concatenated per-stage tables (stage order), see stockham1_stage.
+// In-place FFT of d[fpad(0..n)), n = 2^log2n = nthr * EPT.  stw: per-stage
+// twiddle tables concatenated in stage order (see stockham1_stage).
 template <typename T, bool INV, int EPT>
 __device__ void lds_fft1(cx<T> *d, int log2n, const cx<T> *__restrict__ stw, int tid, int nthr) {
-    int n2, n4, n8;
-    fft1_plan(log2n, &n2, &n4, &n8);
+    int radix[8];
+    const int ns = fft1_plan(log2n, EPT, radix);
     int lns = 0;
     size_t off = 0;
-    for (int s = 0; s < n2; ++s) {
-        stockham1_stage<T, INV, 2, EPT>(d, log2n, lns, stw + off, tid, nthr);
-        off += (size_t)(1 << lns) * 1; lns += 1;
+    for (int st = 0; st < ns; ++st) {
+        const int R = radix[st];
+        if (R == 2) stockham1_stage<T, INV, 2, EPT>(d, log2n, lns, stw + off, tid, nthr);
+        else if (R == 4) stockham1_stage<T, INV, 4, EPT>(d, log2n, lns, stw + off, tid, nthr);
+        else if (R == 8) stockham1_stage<T, INV, 8, EPT>(d, log2n, lns, stw + off, tid, nthr);
+        else if (EPT >= 16) stockham1_stage<T, INV, (EPT >= 16 ? 16 : 8), EPT>(d, log2n, lns, stw + off, tid, nthr);
+        off += (size_t)(1 << lns) * (R - 1);
+        lns += (R == 2) ? 1 : (R == 4) ? 2 : (R == 8) ? 3 : 4;
     }
-    for (int s = 0; s < n4; ++s) {
-        stockham1_stage<T, INV, 4, EPT>(d, log2n, lns, stw + off, tid, nthr);
-        off += (size_t)(1 << lns) * 3; lns += 2;
+}
+
+// ---------------------------------------------------------------------------
+// Compile-time specialisation of lds_fft1 for the hot sizes: every stride and
+// stage offset is a constant, so LDS addresses fold into instruction offsets.
+constexpr int fft1_nstages_ct(int log2n, int ept) {
+    return ept >= 16 ? (log2n / 4 + (log2n % 4 ? 1 : 0))
+                     : (log2n % 3 == 1 && log2n / 3 >= 1 ? log2n / 3 + 1 : log2n / 3 + (log2n % 3 ? 1 : 0));
+}
+constexpr int fft1_radix_ct(int log2n, int ept, int st) {
+    if (ept >= 16) {
+        const int rem = log2n % 4;
+        return (rem && st == 0) ? (1 << rem) : 16;
     }
-    for (int s = 0; s < n8; ++s) {
-        stockham1_stage<T, INV, 8, EPT>(d, log2n, lns, stw + off, tid, nthr);
-        off += (size_t)(1 << lns) * 7; lns += 3;
+    const int rem = log2n % 3;
+    if (rem == 2) return st == 0 ? 4 : 8;
+    if (rem == 1) return (log2n / 3 >= 1) ? (st < 2 ? 4 : 8) : 2;
+    return 8;
+}
+constexpr int fft1_log2ns_ct(int log2n, int ept, int st) {
+    int l = 0;
+    for (int i = 0; i < st; ++i) {
+        const int R = fft1_radix_ct(log2n, ept, i);
+        l += R == 2 ? 1 : R == 4 ? 2 : R == 8 ? 3 : 4;
     }
+    return l;
+}
+constexpr int fft1_off_ct(int log2n, int ept, int st) {
+    int off = 0;
+    for (int i = 0; i < st; ++i) off += (1 << fft1_log2ns_ct(log2n, ept, i)) * (fft1_radix_ct(log2n, ept, i) - 1);
+    return off;
+}
+
+template <typename T, bool INV, int R, int EPT, int LOG2N, int LOG2NS>
+__device__ __forceinline__ void stockham1_stage_ct(cx<T> *d, const cx<T> *__restrict__ stw, int tid) {
+    constexpr int NB = EPT / R;
+    constexpr int LR = (R == 2) ? 1 : (R == 4) ? 2 : (R == 8) ? 3 : 4;
+    constexpr int NBF = 1 << (LOG2N - LR);
+    constexpr int NS = 1 << LOG2NS;
+    constexpr int NTHR = (1 << LOG2N) / EPT;
+    cx<T> v[EPT];
+    int base_out[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        const int j = tid + i * NTHR;
+        const int k = j & (NS - 1);
+        const int jp = fpad(j);
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[i * R + r] = d[(NBF % 16 == 0) ? jp + r * (NBF + NBF / 16) : fpad(j + r * NBF)];
+        if (LOG2NS > 0) {
+#pragma unroll
+            for (int r = 1; r < R; ++r) {
+                cx<T> w = stw[k * (R - 1) + r - 1];
+                if (INV) w.y = -w.y;
+                v[i * R + r] = cmul(v[i * R + r], w);
+            }
+        }
+        dftR<T, INV, R>(&v[i * R]);
+        base_out[i] = ((j - k) << LR) + k;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        const int bp = fpad(base_out[i]);
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            d[(NS % 16 == 0) ? bp + r * (NS + NS / 16) : fpad(base_out[i] + r * NS)] = v[i * R + r];
+    }
+    __syncthreads();
+}
+
+template <typename T, bool INV, int EPT, int LOG2N, int ST>
+__device__ __forceinline__ void lds_fft1_ct_from(cx<T> *d, const cx<T> *__restrict__ stw, int tid) {
+    if constexpr (ST < fft1_nstages_ct(LOG2N, EPT)) {
+        constexpr int R = fft1_radix_ct(LOG2N, EPT, ST);
+        stockham1_stage_ct<T, INV, R, EPT, LOG2N, fft1_log2ns_ct(LOG2N, EPT, ST)>(
+            d, stw + fft1_off_ct(LOG2N, EPT, ST), tid);
+        lds_fft1_ct_from<T, INV, EPT, LOG2N, ST + 1>(d, stw, tid);
+    }
+}
+
+template <typename T, bool INV, int EPT, int LOG2N>
+__device__ __forceinline__ void lds_fft1_ct(cx<T> *d, const cx<T> *__restrict__ stw, int tid) {
+    lds_fft1_ct_from<T, INV, EPT, LOG2N, 0>(d, stw, tid);
 }
 
 }  // namespace sg
