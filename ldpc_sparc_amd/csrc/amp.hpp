@@ -90,8 +90,7 @@ struct RegTables {
     const int32_t *gi;       // [nT][nKmax][4] inverse inputs: G[k] = sum c * z[i]/phi
     const cx<T> *gc;         // [nT][nKmax][4]
     const int32_t *cls_ptr;  // [nT][Q+1]
-    const uint16_t *cls_loc; // [nT][Mc] real LDS index 2*m1 + component
-    const uint16_t *cls_sec; // [nT][Mc] section within the block
+    const uint32_t *cls_ls;  // [nT][Mc] padded real LDS index | section within the block << 16
     const int32_t *cls_j;    // [nT][Mc] column index within the block
     const int32_t *qpos;     // [nT][Mc] column index -> class-order position
     const uint16_t *seg;     // [nT][Q][Lblk+1] section segments within a class

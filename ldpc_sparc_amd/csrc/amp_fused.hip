@@ -63,7 +63,8 @@ __device__ __forceinline__ double reg_block_sum(double v, double *red) {
 constexpr int REG_CH = 8;  // entries a thread loads before using them
 
 size_t reg_stage1_lds(int P, int Lblk, size_t real_bytes) {
-    return (size_t)(P + (P >> 4)) * 2 * real_bytes + (size_t)2 * Lblk * real_bytes;
+    return (size_t)(P + (P >> 4)) * 2 * real_bytes + (size_t)2 * Lblk * real_bytes +
+           (size_t)(64 + (P + 63) / 64) * 2 * real_bytes;
 }
 
 // ------------------------------------------------------------------ ab stage 1
@@ -75,10 +76,14 @@ __global__ __launch_bounds__(1024) void reg_ab_stage1(RegTables<T> tb, RegBufs<T
     const int Pp = tb.P + (tb.P >> 4);  // padded FFT array (fpad)
     T *sM = dr + 2 * (size_t)Pp;
     T *sI = sM + tb.Lblk;
+    cx<T> *ta = reinterpret_cast<cx<T> *>(sI + tb.Lblk);  // w_N2^(m2 k1) factors of this class
+    cx<T> *tbb = ta + 64;
     const int m2 = blockIdx.x, t = blockIdx.y, cw = blockIdx.z;
     if (bf.mode == 0 && !bf.active[cw] && !tb.skip) return;
     const int tid = threadIdx.x, nthr = blockDim.x;
     for (int i = tid; i < 2 * Pp; i += nthr) dr[i] = T(0);
+    for (int i = tid; i < 64 + tb.nB; i += nthr)
+        ta[i] = i < 64 ? tb.twa[m2 * 64 + i] : tb.twb[m2 * tb.nB + i - 64];
     const size_t tc = (size_t)t * tb.Mc;
     T tau = T(1), inv_tau = T(1);
     if (bf.mode == 0) {
@@ -94,31 +99,31 @@ __global__ __launch_bounds__(1024) void reg_ab_stage1(RegTables<T> tb, RegBufs<T
     __syncthreads();
     const int32_t *cp = tb.cls_ptr + (size_t)t * (tb.Q + 1);
     const int q0 = cp[m2], q1 = cp[m2 + 1];
-    const uint16_t *loc = tb.cls_loc + tc;
+    const uint32_t *ls = tb.cls_ls + tc;
     if (bf.mode == 0 && !(tb.skip & 2)) {
         const T *s = bf.s + (size_t)cw * tb.LM + tc;
-        const uint16_t *sec = tb.cls_sec + tc;
         for (int base = q0 + tid; base < q1; base += REG_CH * nthr) {
             T v[REG_CH];
-            int lc[REG_CH], sc[REG_CH];
+            uint32_t e[REG_CH];
 #pragma unroll
             for (int i = 0; i < REG_CH; ++i) {  // issue every load of the chunk first
                 const int q = base + i * nthr;
                 if (q < q1) {
                     v[i] = s[q];
-                    lc[i] = loc[q];
-                    sc[i] = sec[q];
+                    e[i] = ls[q];
                 }
             }
 #pragma unroll
             for (int i = 0; i < REG_CH; ++i)
-                if (base + i * nthr < q1)
-                    dr[lc[i]] = rexp<T>(sm_arg<T>(v[i], sM[sc[i]], tau, inv_tau)) * sI[sc[i]];
+                if (base + i * nthr < q1) {
+                    const int l = e[i] >> 16;
+                    dr[e[i] & 0xffffu] = rexp<T>(sm_arg<T>(v[i], sM[l], tau, inv_tau)) * sI[l];
+                }
         }
     } else if (bf.mode != 0) {
         const T *x = bf.ext_in + (size_t)cw * tb.LM + tc;
         const int32_t *cj = tb.cls_j + tc;
-        for (int q = q0 + tid; q < q1; q += nthr) dr[loc[q]] = x[cj[q]];
+        for (int q = q0 + tid; q < q1; q += nthr) dr[ls[q] & 0xffffu] = x[cj[q]];
     }
     __syncthreads();
     if (!(tb.skip & 1)) {
@@ -128,21 +133,17 @@ __global__ __launch_bounds__(1024) void reg_ab_stage1(RegTables<T> tb, RegBufs<T
     const int nR = (tb.skip & 4) ? 0 : tb.nR[t];
     const int32_t *rk = tb.row_k1 + (size_t)t * tb.nRmax;
     cx<T> *out = bf.tu + (((size_t)cw * tb.nT + t) * tb.Q + m2) * tb.nRmax;
-    for (int base = tid; base < nR; base += REG_CH * nthr) {
-        int k1[REG_CH];
-        cx<T> w[REG_CH];
+    // at most P = EPT * nthr rows: every row index is loaded before any store
+    int k1[EPT];
 #pragma unroll
-        for (int i = 0; i < REG_CH; ++i) {
-            const int r = base + i * nthr;
-            k1[i] = r < nR ? rk[r] : 0;
-        }
+    for (int i = 0; i < EPT; ++i) {
+        const int r = tid + i * nthr;
+        k1[i] = r < nR ? rk[r] : 0;
+    }
 #pragma unroll
-        for (int i = 0; i < REG_CH; ++i) w[i] = reg_tw2(tb, m2, k1[i]);
-#pragma unroll
-        for (int i = 0; i < REG_CH; ++i) {
-            const int r = base + i * nthr;
-            if (r < nR) out[r] = cmul(d[fpad(k1[i])], w[i]);
-        }
+    for (int i = 0; i < EPT; ++i) {
+        const int r = tid + i * nthr;
+        if (r < nR) out[r] = cmul(d[fpad(k1[i])], cmul(ta[k1[i] & 63], tbb[k1[i] >> 6]));
     }
 }
 
@@ -330,17 +331,16 @@ __global__ __launch_bounds__(1024) void reg_az_stage2(RegTables<T> tb, RegBufs<T
     const size_t tc = (size_t)t * tb.Mc;
     const int32_t *cp = tb.cls_ptr + (size_t)t * (tb.Q + 1);
     const int q0 = cp[m2], q1 = cp[m2 + 1];
-    const uint16_t *loc = tb.cls_loc + tc;
+    const uint32_t *ls = tb.cls_ls + tc;
     if (bf.mode != 0) {
         T *out = bf.ext_out + (size_t)cw * tb.LM + tc;
         const int32_t *cj = tb.cls_j + tc;
-        for (int q = q0 + tid; q < q1; q += nthr) out[cj[q]] = dr[loc[q]];
+        for (int q = q0 + tid; q < q1; q += nthr) out[cj[q]] = dr[ls[q] & 0xffffu];
         return;
     }
     const double tv = bf.tau[(size_t)cw * tb.Lc + t];
     const T tau = (T)tv, inv_tau = (T)(1.0 / tv);
     T *s = bf.s + (size_t)cw * tb.LM + tc;
-    const uint16_t *sec = tb.cls_sec + tc;
     // s = beta + tau * Az(z/phi) for the thread's entries (a class holds at
     // most 2P = 2 EPT nthr entries); kept in registers until every u is read
     T snv[2 * EPT];
@@ -348,16 +348,13 @@ __global__ __launch_bounds__(1024) void reg_az_stage2(RegTables<T> tb, RegBufs<T
 #pragma unroll
     for (int c = 0; c < 2 * EPT; c += REG_CH) {
         T v[REG_CH];
-        int lc[REG_CH], sc[REG_CH];
+        uint32_t e[REG_CH];
 #pragma unroll
         for (int i = 0; i < REG_CH; ++i) {
             const int q = q0 + tid + (c + i) * nthr;
             if (q < qe) {
-                lc[i] = loc[q];
-                if (have_beta) {
-                    v[i] = s[q];
-                    sc[i] = sec[q];
-                }
+                e[i] = ls[q];
+                if (have_beta) v[i] = s[q];
             }
         }
 #pragma unroll
@@ -365,10 +362,9 @@ __global__ __launch_bounds__(1024) void reg_az_stage2(RegTables<T> tb, RegBufs<T
             const int q = q0 + tid + (c + i) * nthr;
             if (q < qe) {
                 T b = T(0);
-                if (have_beta) b = rexp<T>(sm_arg<T>(v[i], sM[sc[i]], tp, inv_tp)) * sI[sc[i]];
-                const T sn = b + tau * dr[lc[i]];
-                s[q] = sn;
-                snv[c + i] = sn;
+                const int l = e[i] >> 16;
+                if (have_beta) b = rexp<T>(sm_arg<T>(v[i], sM[l], tp, inv_tp)) * sI[l];
+                snv[c + i] = b + tau * dr[e[i] & 0xffffu];
             }
         }
     }
@@ -384,20 +380,40 @@ __global__ __launch_bounds__(1024) void reg_az_stage2(RegTables<T> tb, RegBufs<T
     T *pm = bf.part + (((size_t)cw * tb.nT + t) * tb.Q + m2) * 3 * (size_t)tb.Lblk;
     // one thread per section over its contiguous segment (segments average
     // ~16 entries: the fpad skew spreads the threads over the LDS banks)
+    constexpr int RC = 16;  // LDS reads in flight per thread
     for (int l = tid; l < tb.Lblk; l += nthr) {
         const int a = sg[l], b = sg[l + 1];
         T m = -INFINITY;
-        for (int q = a; q < b; ++q) m = fmax(m, dr[fpad(q)]);
+        for (int c = a; c < b; c += RC) {
+            T v[RC];
+#pragma unroll
+            for (int i = 0; i < RC; ++i) {
+                const T x = dr[fpad(c + i)];  // in bounds of the LDS image; masked below
+                v[i] = (c + i < b) ? x : T(-INFINITY);
+            }
+#pragma unroll
+            for (int i = 0; i < RC; ++i) m = fmax(m, v[i]);
+        }
         T S1 = T(0), S2 = T(0);
-        for (int q = a; q < b; ++q) {
-            const T e = rexp<T>(sm_arg<T>(dr[fpad(q)], m, tau, inv_tau));
-            S1 += e;
-            S2 += e * e;
+        for (int c = a; c < b; c += RC) {
+            T v[RC];
+#pragma unroll
+            for (int i = 0; i < RC; ++i) v[i] = dr[fpad(c + i)];
+#pragma unroll
+            for (int i = 0; i < RC; ++i)
+                if (c + i < b) {
+                    const T e = rexp<T>(sm_arg<T>(v[i], m, tau, inv_tau));
+                    S1 += e;
+                    S2 += e * e;
+                }
         }
         pm[l] = m;
         pm[tb.Lblk + l] = S1;
         pm[2 * tb.Lblk + l] = S2;
     }
+    // s to HBM last (from the class-ordered LDS copy): stores count in vmcnt,
+    // so they stay out of the load loops
+    for (int q = q0 + tid; q < qe; q += nthr) s[q] = dr[fpad(q - q0)];
 }
 
 // ------------------------------------------------------------------ control
@@ -542,10 +558,10 @@ __global__ __launch_bounds__(256) void reg_map(RegTables<T> tb, RegBufs<T> bf) {
     const int32_t *cp = tb.cls_ptr + (size_t)t * (tb.Q + 1);
     const int q0 = cp[m2], q1 = cp[m2 + 1];
     const T *s = bf.s + (size_t)cw * tb.LM + tc;
-    const uint16_t *sec = tb.cls_sec + tc;
+    const uint32_t *lsq = tb.cls_ls + tc;
     const int32_t *cj = tb.cls_j + tc;
     for (int q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
-        const int ls = sec[q];
+        const int ls = lsq[q] >> 16;
         const size_t l = (size_t)cw * tb.L + (size_t)t * tb.Lblk + ls;
         if (s[q] == bf.stM[l]) atomicMin(&bf.map[l], cj[q] - ls * tb.M);
     }

@@ -41,7 +41,8 @@ struct sg_amp_plan {
     int32_t *r_nR = nullptr, *r_row_k1 = nullptr, *r_kptr = nullptr, *r_kk2 = nullptr, *r_krho = nullptr;
     int32_t *r_oa = nullptr, *r_ob = nullptr, *r_gi = nullptr, *r_cls_ptr = nullptr, *r_cls_j = nullptr,
             *r_qpos = nullptr;
-    uint16_t *r_cls_loc = nullptr, *r_cls_sec = nullptr, *r_seg = nullptr;
+    uint32_t *r_cls_ls = nullptr;
+    uint16_t *r_seg = nullptr;
     void *r_oc = nullptr, *r_gc = nullptr, *r_twP = nullptr, *r_twQ = nullptr, *r_stw = nullptr, *r_twa = nullptr,
          *r_twb = nullptr;
     void *ws_s = nullptr, *ws_tu = nullptr, *ws_xn = nullptr, *ws_part = nullptr, *ws_stM = nullptr,
@@ -239,7 +240,8 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
     std::vector<std::vector<int32_t>> row_k1(nT), kptr(nT), kk2(nT), krho(nT), oa(nT), ob(nT), gi(nT);
     std::vector<std::vector<cd>> oc(nT), gc(nT);
     std::vector<int32_t> cls_ptr((size_t)nT * (Q + 1)), cls_j((size_t)nT * Mc), qpos((size_t)nT * Mc);
-    std::vector<uint16_t> cls_loc((size_t)nT * Mc), cls_sec((size_t)nT * Mc), seg((size_t)nT * Q * (Lblk + 1));
+    std::vector<uint16_t> cls_sec((size_t)nT * Mc), seg((size_t)nT * Q * (Lblk + 1));
+    std::vector<uint32_t> cls_ls((size_t)nT * Mc);
     std::vector<int32_t> kidx(N2, -1);
     std::vector<uint8_t> used(N), need(N2);
     for (int t = 0; t < nT; ++t) {
@@ -265,8 +267,8 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
         for (int j = 0; j < Mc; ++j) {  // ascending j: each class sorted by (section, j)
             const int q = fill[m2of[j]]++;
             const size_t o = (size_t)t * Mc + q;
-            cls_loc[o] = (uint16_t)locof[j];
             cls_sec[o] = (uint16_t)(j / M);
+            cls_ls[o] = (uint32_t)locof[j] | ((uint32_t)(j / M) << 16);
             cls_j[o] = j;
             qpos[(size_t)t * Mc + j] = q;
         }
@@ -404,8 +406,7 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
     SG_TRY(upload(p, &p->r_gi, f_gi));
     SG_TRY(upload_cx(p, &p->r_gc, f_gc));
     SG_TRY(upload(p, &p->r_cls_ptr, cls_ptr));
-    SG_TRY(upload(p, &p->r_cls_loc, cls_loc));
-    SG_TRY(upload(p, &p->r_cls_sec, cls_sec));
+    SG_TRY(upload(p, &p->r_cls_ls, cls_ls));
     SG_TRY(upload(p, &p->r_cls_j, cls_j));
     SG_TRY(upload(p, &p->r_qpos, qpos));
     SG_TRY(upload(p, &p->r_seg, seg));
@@ -425,7 +426,7 @@ static RegTables<T> rtables(const sg_amp_plan *p) {
     tb.nRmax = p->nRmax; tb.nKmax = p->nKmax; tb.RB = p->RB; tb.nrb = p->nrb; tb.maxKb = p->maxKb;
     tb.nR = p->r_nR; tb.row_k1 = p->r_row_k1; tb.kptr = p->r_kptr; tb.kk2 = p->r_kk2; tb.krho = p->r_krho;
     tb.oa = p->r_oa; tb.ob = p->r_ob; tb.oc = (const cx<T> *)p->r_oc; tb.gi = p->r_gi; tb.gc = (const cx<T> *)p->r_gc;
-    tb.cls_ptr = p->r_cls_ptr; tb.cls_loc = p->r_cls_loc; tb.cls_sec = p->r_cls_sec; tb.cls_j = p->r_cls_j;
+    tb.cls_ptr = p->r_cls_ptr; tb.cls_ls = p->r_cls_ls; tb.cls_j = p->r_cls_j;
     tb.qpos = p->r_qpos; tb.seg = p->r_seg;
     tb.twP = (const cx<T> *)p->r_twP; tb.twQ = (const cx<T> *)p->r_twQ;
     tb.twHi = (const cx<T> *)p->twHi; tb.twLo = (const cx<T> *)p->twLo;
