@@ -74,6 +74,42 @@ int sg_profile_enable(int on);
 int sg_profile_collect(double *total_ms, int64_t *launches);
 const char *sg_phase_name(int phase);
 
+/* ------------------------------------------------------- dense design AMP */
+typedef struct sg_dense_plan sg_dense_plan;
+
+/* Dense Gaussian design A [n][L*M] row-major (create_design_matrix,
+ * sparc_new.py:1284-1294: default_rng(seed).normal(0, 1/sqrt(n))), uploaded
+ * once and shared by every codeword of a batch.  P is the total power
+ * (nonzero entries sqrt(n P / L), sparc_new.py:45-46).  SG_F32 runs the two
+ * products as matrix-core GEMMs (v_mfma_f32_32x32x2_f32); SG_F64 is the
+ * parity path.  _random draws A on the device (Philox4x32-10 + Box-Muller,
+ * statistically equal to the reference's draw, not bitwise) for throughput runs. */
+int sg_dense_plan_create(const double *A, int n, int L, int M, double P, int precision, sg_dense_plan **out);
+int sg_dense_plan_create_random(int n, int L, int M, double P, uint64_t seed, int precision,
+                                sg_dense_plan **out);
+int sg_dense_plan_destroy(sg_dense_plan *p);
+int sg_dense_plan_info(const sg_dense_plan *p, int *n, int *L, int *M, int *nsplit);
+/* Batched AMP with fixed t_max iterations (sparc_new.py:885-912, one call per
+ * codeword in the reference): y [B][n] -> soft estimate beta [B][L*M] and
+ * effective observation s [B][L*M] (the reference's return values). */
+int sg_dense_amp(sg_dense_plan *p, const double *y, int B, int t_max, double *beta, double *s);
+int sg_dense_amp_device(sg_dense_plan *p, const void *d_y, int B, int t_max, void *d_beta, void *d_s,
+                        void *stream);
+/* One iteration from a given state (sparc_amp_single_it, sparc_new.py:975-990):
+ * y [n], beta [L*M], z [n], tau_sqr -> beta', z', tau_sqr'. */
+int sg_dense_amp_iteration(sg_dense_plan *p, const double *y, const double *beta, const double *z,
+                           double tau_sqr, double *beta_out, double *z_out, double *tau_sqr_out);
+/* x = A beta0 for one-hot beta0 (section index d_idx [B][L], value sqrt(n P / L)). */
+int sg_dense_encode_device(sg_dense_plan *p, const int32_t *d_idx, int B, void *d_x, void *stream);
+/* MAP section indices of s [B][L*M] (msg_vector_map_estimator, sparc_new.py:1099-1116). */
+int sg_dense_map_device(sg_dense_plan *p, const void *d_s, int B, int32_t *d_idx, void *stream);
+/* AMP -> BP glue (beta_estimate_to_bp_probs, sparc_new.py:1118-1138, then the
+ * clip and log of ldpc_bp :1167-1169): for sections [l0, l0+nl) of beta
+ * [B][L*M], bit LLRs (MSB first, positive => 0) at d_llr[b*llr_ld + (l-l0)*log2 M + i],
+ * or the bit-0 probabilities themselves when probs_only. */
+int sg_beta_to_llr_device(int precision, const void *d_beta, int B, int L, int M, double sqrt_nPl, int l0,
+                          int nl, int llr_ld, int probs_only, void *d_llr, void *stream);
+
 /* ------------------------------------------------------------- multi-GPU */
 /* One RCCL communicator per process (one process per GPU).  Rank 0 creates
  * the 128-byte unique id, the launcher distributes it, every rank calls init.

@@ -84,6 +84,19 @@ SIGNATURES = [
     ("sg_comm_init", ct.c_int, [ct.c_int, ct.c_int, vp, ct.POINTER(vp)]),
     ("sg_comm_allreduce_sum_i64", ct.c_int, [vp, vp, ct.c_size_t, vp]),
     ("sg_comm_destroy", ct.c_int, [vp]),
+    ("sg_dense_plan_create", ct.c_int, [vp, ct.c_int, ct.c_int, ct.c_int, ct.c_double, ct.c_int,
+                                        ct.POINTER(vp)]),
+    ("sg_dense_plan_create_random", ct.c_int, [ct.c_int, ct.c_int, ct.c_int, ct.c_double, ct.c_uint64,
+                                               ct.c_int, ct.POINTER(vp)]),
+    ("sg_dense_plan_destroy", ct.c_int, [vp]),
+    ("sg_dense_plan_info", ct.c_int, [vp] + [ct.POINTER(ct.c_int)] * 4),
+    ("sg_dense_amp", ct.c_int, [vp, vp, ct.c_int, ct.c_int, vp, vp]),
+    ("sg_dense_amp_device", ct.c_int, [vp, vp, ct.c_int, ct.c_int, vp, vp, vp]),
+    ("sg_dense_amp_iteration", ct.c_int, [vp, vp, vp, vp, ct.c_double, vp, vp, vp]),
+    ("sg_dense_encode_device", ct.c_int, [vp, vp, ct.c_int, vp, vp]),
+    ("sg_dense_map_device", ct.c_int, [vp, vp, ct.c_int, vp, vp]),
+    ("sg_beta_to_llr_device", ct.c_int, [ct.c_int, vp, ct.c_int, ct.c_int, ct.c_int, ct.c_double, ct.c_int,
+                                         ct.c_int, ct.c_int, ct.c_int, vp, vp]),
 ]
 
 SG_PH_COUNT = 8

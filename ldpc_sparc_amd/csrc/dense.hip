@@ -1,0 +1,456 @@
+// Dense Gaussian-design AMP on gfx950 (sparc_sophie/sparc_new.py:885-912,
+// msg_vector_mmse_estimator :1040-1066, MAP :1099-1116) and the AMP -> BP
+// glue (beta_estimate_to_bp_probs :1118-1138, ldpc_bp :1167-1169).
+//
+// A batch of B codewords shares the design matrix A [n][LM], so the two
+// matrix-vector products of the reference become GEMMs on the matrix cores:
+//   A beta   : C[B][n]  = beta[B][LM] . A[n][LM]^T   (split over K = LM)
+//   A^T z    : C[B][LM] = z[B][npad]  . A[n][LM]     (epilogue s = beta + C)
+// f32 uses v_mfma_f32_32x32x2_f32 (exact f32 FMA chains); f64 (parity mode,
+// small designs) uses plain FMA kernels.
+#include "dense.hpp"
+
+namespace sg {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// ------------------------------------------------------------------ f32 MFMA GEMM
+// C[M][N] (+)= X[M][K] . Y, X K-contiguous; Y = [N][K] (NT) or [K][N] (NN).
+// 128 x 128 x 32 block tile, 4 waves in 2 x 2, each 64 x 64 = 2 x 2 MFMA tiles.
+struct GemmF32 {
+    const float *X;
+    long ldx;
+    const float *Y;
+    long ldy;
+    float *C;
+    long ldc;
+    const float *add;  // NN epilogue: C = add + acc (same layout as C), or null
+    long c_split;      // NT: split z writes C + z * c_split
+    int M, N, K, kchunk, yrows;  // yrows: rows of Y (N for NT, K rows for NN) that exist
+};
+
+constexpr int GBM = 128, GBN = 128, GBK = 32, GPAD = GBK + 1;
+
+template <bool NT>
+__global__ __launch_bounds__(256) void gemm_f32_mfma(GemmF32 g) {
+    __shared__ float Xs[GBM * GPAD];
+    __shared__ float Ys[NT ? GBN * GPAD : GBK * GBN];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+    const int m0 = blockIdx.y * GBM, n0 = blockIdx.x * GBN;
+    const int kb = blockIdx.z * g.kchunk;
+    const int ke = min(g.K, kb + g.kchunk);
+    const int nk = (ke - kb + GBK - 1) / GBK;
+    float4 xr[4], yr[4];
+    auto load = [&](int k0) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int f = tid + 256 * p;
+            const int r = f >> 3, c = (f & 7) * 4;
+            const int m = m0 + r;
+            xr[p] = (m < g.M && k0 + c < ke) ? *reinterpret_cast<const float4 *>(g.X + (long)m * g.ldx + k0 + c)
+                                             : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (NT) {
+                const int nn = n0 + r;
+                yr[p] = (nn < g.yrows && k0 + c < ke)
+                            ? *reinterpret_cast<const float4 *>(g.Y + (long)nn * g.ldy + k0 + c)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+            } else {
+                const int r2 = f >> 5, c2 = (f & 31) * 4;
+                const int kk = k0 + r2, nn = n0 + c2;
+                yr[p] = (kk < ke && kk < g.yrows && nn < g.N)
+                            ? *reinterpret_cast<const float4 *>(g.Y + (long)kk * g.ldy + nn)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+    };
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+    if (nk > 0) load(kb);
+    for (int kt = 0; kt < nk; ++kt) {
+        __syncthreads();
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int f = tid + 256 * p;
+            const int r = f >> 3, c = (f & 7) * 4;
+            float *xd = Xs + r * GPAD + c;
+            xd[0] = xr[p].x; xd[1] = xr[p].y; xd[2] = xr[p].z; xd[3] = xr[p].w;
+            if (NT) {
+                float *yd = Ys + r * GPAD + c;
+                yd[0] = yr[p].x; yd[1] = yr[p].y; yd[2] = yr[p].z; yd[3] = yr[p].w;
+            } else {
+                const int r2 = f >> 5, c2 = (f & 31) * 4;
+                *reinterpret_cast<float4 *>(Ys + r2 * GBN + c2) = yr[p];
+            }
+        }
+        __syncthreads();
+        if (kt + 1 < nk) load(kb + (kt + 1) * GBK);  // next tile in flight during the MFMAs
+#pragma unroll
+        for (int kk = 0; kk < GBK / 2; ++kk) {
+            const int kx = 2 * kk + (lane >> 5);
+            float a[2], b[2];
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) a[mt] = Xs[(wm * 64 + mt * 32 + (lane & 31)) * GPAD + kx];
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt)
+                b[nt] = NT ? Ys[(wn * 64 + nt * 32 + (lane & 31)) * GPAD + kx]
+                           : Ys[kx * GBN + wn * 64 + nt * 32 + (lane & 31)];
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt)
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
+        }
+    }
+    float *C = g.C + (long)blockIdx.z * g.c_split;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + wm * 64 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                const int col = n0 + wn * 64 + nt * 32 + (lane & 31);
+                if (row < g.M && col < g.N) {
+                    const long o = (long)row * g.ldc + col;
+                    C[o] = g.add ? g.add[o] + acc[mt][nt][r] : acc[mt][nt][r];
+                }
+            }
+}
+
+// ------------------------------------------------------------------ f64 (parity) products
+// part[0][b][i] = sum_j A[i][j] beta[b][j]: one workgroup per row i.
+__global__ __launch_bounds__(256) void ab_f64_kernel(const double *__restrict__ A, const double *__restrict__ beta,
+                                                     int n, int LM, int B, double *__restrict__ out) {
+    __shared__ double red[4][8];
+    const int i = blockIdx.x, tid = threadIdx.x;
+    const double *Ai = A + (long)i * LM;
+    for (int b0 = 0; b0 < B; b0 += 8) {
+        double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int j = tid; j < LM; j += 256) {
+            const double a = Ai[j];
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (b0 + q < B) acc[q] += a * beta[(long)(b0 + q) * LM + j];
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            double v = acc[q];
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            if ((tid & 63) == 0) red[tid >> 6][q] = v;
+        }
+        __syncthreads();
+        if (tid < 8 && b0 + tid < B)
+            out[(long)(b0 + tid) * n + i] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+        __syncthreads();
+    }
+}
+
+// s[b][j] = beta[b][j] + sum_i A[i][j] z[b][i]
+__global__ __launch_bounds__(256) void az_f64_kernel(const double *__restrict__ A, const double *__restrict__ z,
+                                                     const double *__restrict__ beta, int n, int npad, int LM,
+                                                     double *__restrict__ s) {
+    const int b = blockIdx.y;
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= LM) return;
+    double acc = 0.0;
+    for (int i = 0; i < n; ++i) acc += A[(long)i * LM + j] * z[(long)b * npad + i];
+    s[(long)b * LM + j] = beta[(long)b * LM + j] + acc;
+}
+
+// ------------------------------------------------------------------ residual
+// t > 0: z = y - A beta + (z / tau^2)(P - ||beta||^2 / n)   (sparc_new.py:902-905)
+// t = 0: z = y.  Also writes per-block partial sums of z^2 for tau^2.
+template <typename T>
+__global__ __launch_bounds__(256) void residual_kernel(DenseBufs<T> d, int t, double *z2part, int nblk) {
+    __shared__ double red[4];
+    __shared__ double sh_bsq;
+    const int b = blockIdx.y, tid = threadIdx.x;
+    const int i = blockIdx.x * 256 + tid;
+    if (t > 0 && tid < 64) {  // ||beta||^2 of the codeword, fixed order
+        double v = 0.0;
+        for (int l = tid; l < d.L; l += 64) v += d.sec_bsq[(long)b * d.L + l];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (tid == 0) sh_bsq = v;
+    }
+    __syncthreads();
+    double zz = 0.0;
+    if (i < d.npad) {
+        T zn = T(0);
+        if (i < d.n) {
+            const T y = d.y[(long)b * d.n + i];
+            if (t > 0) {
+                T r = T(0);
+                for (int sp = 0; sp < d.nsplit; ++sp) r += d.part[((long)sp * d.B + b) * d.n + i];
+                const T zo = d.z[(long)b * d.npad + i];
+                const T ons = (zo / (T)d.tau2[b]) * (T)(d.P - sh_bsq / d.n);
+                zn = (y - r) + ons;
+            } else {
+                zn = y;
+            }
+        }
+        d.z[(long)b * d.npad + i] = zn;
+        zz = (double)zn * (double)zn;
+    }
+    for (int o = 32; o > 0; o >>= 1) zz += __shfl_xor(zz, o, 64);
+    if ((tid & 63) == 0) red[tid >> 6] = zz;
+    __syncthreads();
+    if (tid == 0) z2part[(long)b * nblk + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void tau2_kernel(const double *z2part, int nblk, int n, double *tau2) {
+    const int b = blockIdx.x;
+    if (threadIdx.x == 0) {
+        double v = 0.0;
+        for (int k = 0; k < nblk; ++k) v += z2part[(long)b * nblk + k];
+        tau2[b] = v / n;  // tau_sqr = sum(z^2) / n (sparc_new.py:908)
+    }
+}
+
+// ------------------------------------------------------------------ eta
+// beta = sqrt(n P_l) softmax(sqrt(n P_l) s / tau^2) per section (sparc_new.py:1058-1066,
+// per-section maximum: same value as the reference's global shift), and the
+// section's sum of beta^2.  One wavefront per section.
+template <typename T>
+__device__ __forceinline__ T dexp2(T x);
+template <>
+__device__ __forceinline__ float dexp2<float>(float x) { return __expf(x); }
+template <>
+__device__ __forceinline__ double dexp2<double>(double x) { return exp(x); }
+
+template <typename T>
+__global__ __launch_bounds__(256) void dense_eta_kernel(DenseBufs<T> d) {
+    const int lane = threadIdx.x & 63;
+    const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int b = blockIdx.y;
+    if (l >= d.L) return;
+    const double snp = sqrt((double)d.n * (d.P / d.L));
+    const T c = (T)snp, tau2 = (T)d.tau2[b];
+    const T *s = d.s + (long)b * d.LM + (long)l * d.M;
+    T *beta = d.beta + (long)b * d.LM + (long)l * d.M;
+    T mx = -INFINITY;
+    for (int j = lane; j < d.M; j += 64) mx = fmax(mx, c * (s[j] / tau2));
+    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+    T den = T(0);
+    for (int j = lane; j < d.M; j += 64) den += dexp2<T>(c * (s[j] / tau2) - mx);
+    for (int o = 32; o > 0; o >>= 1) den += __shfl_xor(den, o, 64);
+    double sq = 0.0;
+    for (int j = lane; j < d.M; j += 64) {
+        const T v = c * (dexp2<T>(c * (s[j] / tau2) - mx) / den);
+        beta[j] = v;
+        sq += (double)v * (double)v;
+    }
+    for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
+    if (lane == 0) d.sec_bsq[(long)b * d.L + l] = sq;
+}
+
+// Per-section sum of beta^2 of a given beta (state handed in by the caller).
+template <typename T>
+__global__ __launch_bounds__(256) void dense_bsq_kernel(DenseBufs<T> d) {
+    const int lane = threadIdx.x & 63;
+    const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int b = blockIdx.y;
+    if (l >= d.L) return;
+    const T *beta = d.beta + (long)b * d.LM + (long)l * d.M;
+    double sq = 0.0;
+    for (int j = lane; j < d.M; j += 64) sq += (double)beta[j] * (double)beta[j];
+    for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
+    if (lane == 0) d.sec_bsq[(long)b * d.L + l] = sq;
+}
+
+template <typename T>
+int dense_launch_bsq(const DenseBufs<T> &d, hipStream_t s) {
+    hipLaunchKernelGGL((dense_bsq_kernel<T>), dim3((d.L + 3) / 4, d.B), dim3(256), 0, s, d);
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
+// MAP: first index of the section maximum of s (numpy argmax).
+template <typename T>
+__global__ __launch_bounds__(256) void dense_map_kernel(const T *s, int B, int L, int M, int32_t *idx) {
+    const int lane = threadIdx.x & 63;
+    const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int b = blockIdx.y;
+    if (l >= L) return;
+    const T *ss = s + (long)b * L * M + (long)l * M;
+    T best = -INFINITY;
+    int arg = 0x7fffffff;
+    for (int j = lane; j < M; j += 64)
+        if (arg == 0x7fffffff || ss[j] > best) { best = ss[j]; arg = j; }
+    T g = best;
+    for (int o = 32; o > 0; o >>= 1) g = fmax(g, __shfl_xor(g, o, 64));
+    int cand = (best == g) ? arg : 0x7fffffff;
+    for (int o = 32; o > 0; o >>= 1) cand = min(cand, __shfl_xor(cand, o, 64));
+    if (lane == 0) idx[(long)b * L + l] = cand == 0x7fffffff ? 0 : cand;
+}
+
+// ------------------------------------------------------------------ glue
+// LLR of each (MSB-first) bit of the protected sections from the soft
+// estimate: p0 = sum over indices whose bit is 0 of beta / sqrt(n P_l),
+// clipped to [1e-15, 1 - 1e-15], LLR = log p0 - log(1 - p0) (positive => 0).
+template <typename T>
+__global__ __launch_bounds__(256) void glue_llr_kernel(const T *beta, int B, int L, int M, int l0, int nl,
+                                                       double inv_snp, int llr_ld, T *llr, int probs_only) {
+    const int lane = threadIdx.x & 63;
+    const int li = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int b = blockIdx.y;
+    if (li >= nl) return;
+    int logM = 0;
+    while ((1 << logM) < M) ++logM;
+    const T *bs = beta + (long)b * L * M + (long)(l0 + li) * M;
+    for (int pos = 0; pos < logM; ++pos) {
+        const int bit = logM - 1 - pos;
+        double p = 0.0;
+        for (int j = lane; j < M; j += 64)
+            if (((j >> bit) & 1) == 0) p += (double)bs[j] * inv_snp;
+        for (int o = 32; o > 0; o >>= 1) p += __shfl_xor(p, o, 64);
+        if (lane == 0) {
+            const double eps = 1e-15;
+            const double pc = fmin(fmax(p, eps), 1.0 - eps);  // ldpc_bp's clip (sparc_new.py:1167)
+            llr[(long)b * llr_ld + (long)li * logM + pos] = probs_only ? (T)p : (T)(log(pc) - log(1.0 - pc));
+        }
+    }
+}
+
+// ------------------------------------------------------------------ random design
+// Throughput mode: A[i][j] ~ N(0, 1/n) from Philox4x32-10 (counter = element
+// index / 4, key = seed) and Box-Muller; statistically, not bitwise, equal to
+// numpy's default_rng(seed).normal (parity mode uploads the reference draw).
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0, h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
+        c[0] = h1 ^ c[1] ^ k0;
+        c[1] = l1;
+        c[2] = h0 ^ c[3] ^ k1;
+        c[3] = l0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
+template <typename T>
+__global__ void gen_A_kernel(T *A, long total, double scale, uint64_t seed) {
+    const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;  // 4 outputs per thread
+    if (q * 4 >= total) return;
+    uint32_t c[4] = {(uint32_t)q, (uint32_t)(q >> 32), 0x5eed5eedu, 0u};
+    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const double two32 = 4294967296.0;
+    float out[4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const double u1 = ((double)c[2 * h] + 1.0) / (two32 + 1.0);
+        const double u2 = (double)c[2 * h + 1] / two32;
+        const double r = sqrt(-2.0 * log(u1));
+        out[2 * h] = (float)(r * cos(2.0 * M_PI * u2));
+        out[2 * h + 1] = (float)(r * sin(2.0 * M_PI * u2));
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+        if (q * 4 + e < total) A[q * 4 + e] = (T)(out[e] * scale);
+}
+
+// ------------------------------------------------------------------ launchers
+template <>
+int dense_launch_ab<float>(const DenseBufs<float> &d, hipStream_t s) {
+    ProfScope ps(SG_PH_DENSE, s);
+    GemmF32 g;
+    g.X = d.beta; g.ldx = d.LM; g.Y = d.A; g.ldy = d.LM; g.C = d.part; g.ldc = d.n; g.add = nullptr;
+    g.c_split = (long)d.B * d.n; g.M = d.B; g.N = d.n; g.K = d.LM; g.yrows = d.n;
+    g.kchunk = ((d.LM + d.nsplit - 1) / d.nsplit + GBK - 1) / GBK * GBK;
+    hipLaunchKernelGGL(gemm_f32_mfma<true>, dim3((d.n + GBN - 1) / GBN, (d.B + GBM - 1) / GBM, d.nsplit), dim3(256),
+                       0, s, g);
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+template <>
+int dense_launch_ab<double>(const DenseBufs<double> &d, hipStream_t s) {
+    ProfScope ps(SG_PH_DENSE, s);
+    hipLaunchKernelGGL(ab_f64_kernel, dim3(d.n), dim3(256), 0, s, d.A, d.beta, d.n, d.LM, d.B, d.part);
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
+template <>
+int dense_launch_az<float>(const DenseBufs<float> &d, hipStream_t s) {
+    ProfScope ps(SG_PH_DENSE, s);
+    GemmF32 g;
+    g.X = d.z; g.ldx = d.npad; g.Y = d.A; g.ldy = d.LM; g.C = d.s; g.ldc = d.LM; g.add = d.beta;
+    g.c_split = 0; g.M = d.B; g.N = d.LM; g.K = d.npad; g.kchunk = d.npad; g.yrows = d.n;
+    hipLaunchKernelGGL(gemm_f32_mfma<false>, dim3((d.LM + GBN - 1) / GBN, (d.B + GBM - 1) / GBM, 1), dim3(256), 0,
+                       s, g);
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+template <>
+int dense_launch_az<double>(const DenseBufs<double> &d, hipStream_t s) {
+    ProfScope ps(SG_PH_DENSE, s);
+    hipLaunchKernelGGL(az_f64_kernel, dim3((d.LM + 255) / 256, d.B), dim3(256), 0, s, d.A, d.z, d.beta, d.n, d.npad,
+                       d.LM, d.s);
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
+template <typename T>
+int dense_launch_residual(const DenseBufs<T> &d, int t, hipStream_t s) {
+    ProfScope ps(SG_PH_CONTROL, s);
+    const int nblk = (d.npad + 255) / 256;
+    double *z2part = d.tau2 + d.B;  // the plan allocates tau2 with B + B * nblk entries
+    hipLaunchKernelGGL((residual_kernel<T>), dim3(nblk, d.B), dim3(256), 0, s, d, t, z2part, nblk);
+    hipLaunchKernelGGL(tau2_kernel, dim3(d.B), dim3(64), 0, s, z2part, nblk, d.n, d.tau2);
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
+template <typename T>
+int dense_launch_eta(const DenseBufs<T> &d, hipStream_t s) {
+    ProfScope ps(SG_PH_ETA, s);
+    hipLaunchKernelGGL((dense_eta_kernel<T>), dim3((d.L + 3) / 4, d.B), dim3(256), 0, s, d);
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
+template <typename T>
+int dense_launch_gen_A(T *A, int n, int LM, uint64_t seed, hipStream_t s) {
+    const long total = (long)n * LM;
+    const long nthr = (total + 3) / 4;
+    hipLaunchKernelGGL((gen_A_kernel<T>), dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, s, A, total,
+                       1.0 / sqrt((double)n), seed);
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
+template <typename T>
+int dense_launch_map(const T *sv, int B, int L, int M, int32_t *idx, hipStream_t s) {
+    hipLaunchKernelGGL((dense_map_kernel<T>), dim3((L + 3) / 4, B), dim3(256), 0, s, sv, B, L, M, idx);
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
+template <typename T>
+int glue_launch_llr(const T *beta, int B, int L, int M, int l0, int nl, double inv_snp, int llr_ld, T *llr,
+                    int probs_only, hipStream_t s) {
+    if (B <= 0 || nl <= 0) return SG_OK;
+    hipLaunchKernelGGL((glue_llr_kernel<T>), dim3((nl + 3) / 4, B), dim3(256), 0, s, beta, B, L, M, l0, nl, inv_snp,
+                       llr_ld, llr, probs_only);
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
+#define SG_DENSE_INST(T)                                                                                        \
+    template int dense_launch_bsq<T>(const DenseBufs<T> &, hipStream_t);                                       \
+    template int dense_launch_residual<T>(const DenseBufs<T> &, int, hipStream_t);                             \
+    template int dense_launch_eta<T>(const DenseBufs<T> &, hipStream_t);                                       \
+    template int dense_launch_gen_A<T>(T *, int, int, uint64_t, hipStream_t);                                  \
+    template int dense_launch_map<T>(const T *, int, int, int, int32_t *, hipStream_t);                        \
+    template int glue_launch_llr<T>(const T *, int, int, int, int, int, double, int, T *, int, hipStream_t);
+SG_DENSE_INST(float)
+SG_DENSE_INST(double)
+
+}  // namespace sg

@@ -1,0 +1,46 @@
+// Dense Gaussian-design AMP (sparc_sophie/sparc_new.py:885-912) and the
+// AMP -> BP glue (sparc_new.py:1118-1193): declarations shared by dense.hip
+// and capi_dense.cpp.
+#pragma once
+#include "common.hpp"
+
+namespace sg {
+
+// Batched dense AMP state.  The design matrix A [n][LM] (row-major, as
+// create_design_matrix draws it, sparc_new.py:1284-1294) is shared by the
+// batch; z is padded to npad = roundup(n, 32) columns (zeros beyond n).
+template <typename T>
+struct DenseBufs {
+    const T *A;        // [n][LM]
+    int n, npad, L, M, LM, B;
+    double P;          // total power; P_l = P / L, sqrt(n P_l) is the nonzero value
+    const T *y;        // [B][n]
+    T *z;              // [B][npad]
+    T *beta;           // [B][LM]
+    T *s;              // [B][LM]
+    T *part;           // [nsplit][B][n] split-K partial sums of A beta
+    int nsplit;
+    double *tau2;      // [B]   ||z||^2 / n
+    double *bsq;       // [B]   ||beta||^2
+    double *sec_bsq;   // [B][L] per-section sum beta^2 (deterministic reduction)
+};
+
+template <typename T>
+int dense_launch_ab(const DenseBufs<T> &b, hipStream_t s);            // part = A beta (split K)
+template <typename T>
+int dense_launch_residual(const DenseBufs<T> &b, int t, hipStream_t s);  // z, tau^2 (sparc_new.py:902-908)
+template <typename T>
+int dense_launch_az(const DenseBufs<T> &b, hipStream_t s);            // s = beta + A^T z
+template <typename T>
+int dense_launch_bsq(const DenseBufs<T> &b, hipStream_t s);           // sec_bsq from a given beta
+template <typename T>
+int dense_launch_eta(const DenseBufs<T> &b, hipStream_t s);           // beta = eta(s), ||beta||^2
+template <typename T>
+int dense_launch_gen_A(T *A, int n, int LM, uint64_t seed, hipStream_t s);  // A ~ N(0, 1/n), Philox
+template <typename T>
+int dense_launch_map(const T *s, int B, int L, int M, int32_t *idx, hipStream_t st);
+template <typename T>
+int glue_launch_llr(const T *beta, int B, int L, int M, int l0, int nl, double inv_sqrt_nPl, int llr_ld, T *llr,
+                    int probs_only, hipStream_t s);
+
+}  // namespace sg
