@@ -110,6 +110,16 @@ int sg_dense_map_device(sg_dense_plan *p, const void *d_s, int B, int32_t *d_idx
 int sg_beta_to_llr_device(int precision, const void *d_beta, int B, int L, int M, double sqrt_nPl, int l0,
                           int nl, int llr_ld, int probs_only, void *d_llr, void *stream);
 
+/* Error counts of the concatenated scheme (sparc_sim_new.py:12-23):
+ * unprotected bits from MAP indices d_map_idx [B][L] (first L_unprotected
+ * sections) against d_true_idx, protected bits app[:K] < 0 of each of the
+ * `mults` BP blocks (d_app [B*mults][N]) against d_info [B][mults*K].  Adds
+ * {codewords, bit errors, codeword errors, unprotected bit errors, protected
+ * bit errors} into d_counts[5]. */
+int sg_concat_count_errors_device(int precision, const int32_t *d_map_idx, const int32_t *d_true_idx, int B,
+                                  int L, int L_unprotected, int logM, const void *d_app, const uint8_t *d_info,
+                                  int mults, int N, int K, int64_t *d_counts, void *stream);
+
 /* ------------------------------------------------------------- multi-GPU */
 /* One RCCL communicator per process (one process per GPU).  Rank 0 creates
  * the 128-byte unique id, the launcher distributes it, every rank calls init.

@@ -361,4 +361,18 @@ int sg_beta_to_llr_device(int precision, const void *d_beta, int B, int L, int M
                                         probs_only, s);
 }
 
+int sg_concat_count_errors_device(int precision, const int32_t *d_map_idx, const int32_t *d_true_idx, int B, int L,
+                                  int L_unprotected, int logM, const void *d_app, const uint8_t *d_info, int mults,
+                                  int N, int K, int64_t *d_counts, void *stream) {
+    SG_CHECK_ARG(d_map_idx && d_true_idx && d_app && d_info && d_counts, "null device buffer");
+    SG_CHECK_ARG(L_unprotected >= 0 && L_unprotected <= L && mults >= 0 && K <= N, "bad lengths");
+    SG_TRY(ensure_device());
+    hipStream_t s = pick_stream(stream);
+    return precision == SG_F64
+               ? concat_launch_count<double>(d_map_idx, d_true_idx, B, L, L_unprotected, logM, (const double *)d_app,
+                                             d_info, mults, N, K, d_counts, s)
+               : concat_launch_count<float>(d_map_idx, d_true_idx, B, L, L_unprotected, logM, (const float *)d_app,
+                                            d_info, mults, N, K, d_counts, s);
+}
+
 }  // extern "C"

@@ -317,6 +317,54 @@ __global__ __launch_bounds__(256) void glue_llr_kernel(const T *beta, int B, int
     }
 }
 
+// ------------------------------------------------------------------ concatenated error counts
+// Per codeword (sparc_sim_new.py:21, bit_err_rate): unprotected bits from the
+// MAP section indices (MSB-first bits of the index, sparc_new.py:1319-1341),
+// protected bits = hard decisions app[:K] < 0 of every LDPC block
+// (sparc_new.py:1185-1187).  Adds {codewords, bit errors, codeword errors,
+// unprotected bit errors, protected bit errors} to counts[5].
+template <typename T>
+__global__ __launch_bounds__(256) void concat_count_kernel(const int32_t *map_idx, const int32_t *true_idx, int L,
+                                                           int L_unp, int logM, const T *app, const uint8_t *info,
+                                                           int mults, int N, int K, unsigned long long *counts) {
+    __shared__ int red[2][4];
+    const int cw = blockIdx.x, tid = threadIdx.x;
+    int eu = 0, ep = 0;
+    const unsigned mask = (1u << logM) - 1u;
+    for (int l = tid; l < L_unp; l += blockDim.x)
+        eu += __popc(((unsigned)map_idx[(long)cw * L + l] ^ (unsigned)true_idx[(long)cw * L + l]) & mask);
+    for (int e = tid; e < mults * K; e += blockDim.x) {
+        const int blk = e / K, v = e - blk * K;
+        const int hard = app[((long)cw * mults + blk) * N + v] < T(0) ? 1 : 0;
+        ep += hard != (int)info[(long)cw * mults * K + e];
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        eu += __shfl_xor(eu, o, 64);
+        ep += __shfl_xor(ep, o, 64);
+    }
+    if ((tid & 63) == 0) { red[0][tid >> 6] = eu; red[1][tid >> 6] = ep; }
+    __syncthreads();
+    if (tid == 0) {
+        int u = 0, q = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { u += red[0][w]; q += red[1][w]; }
+        atomicAdd(&counts[0], 1ull);
+        atomicAdd(&counts[1], (unsigned long long)(u + q));
+        atomicAdd(&counts[2], (unsigned long long)(u + q > 0));
+        atomicAdd(&counts[3], (unsigned long long)u);
+        atomicAdd(&counts[4], (unsigned long long)q);
+    }
+}
+
+template <typename T>
+int concat_launch_count(const int32_t *map_idx, const int32_t *true_idx, int B, int L, int L_unp, int logM,
+                        const T *app, const uint8_t *info, int mults, int N, int K, int64_t *counts, hipStream_t s) {
+    if (B <= 0) return SG_OK;
+    hipLaunchKernelGGL((concat_count_kernel<T>), dim3(B), dim3(256), 0, s, map_idx, true_idx, L, L_unp, logM, app,
+                       info, mults, N, K, reinterpret_cast<unsigned long long *>(counts));
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
 // ------------------------------------------------------------------ random design
 // Throughput mode: A[i][j] ~ N(0, 1/n) from Philox4x32-10 (counter = element
 // index / 4, key = seed) and Box-Muller; statistically, not bitwise, equal to
@@ -445,6 +493,8 @@ int glue_launch_llr(const T *beta, int B, int L, int M, int l0, int nl, double i
 
 #define SG_DENSE_INST(T)                                                                                        \
     template int dense_launch_bsq<T>(const DenseBufs<T> &, hipStream_t);                                       \
+    template int concat_launch_count<T>(const int32_t *, const int32_t *, int, int, int, int, const T *,        \
+                                        const uint8_t *, int, int, int, int64_t *, hipStream_t);              \
     template int dense_launch_residual<T>(const DenseBufs<T> &, int, hipStream_t);                             \
     template int dense_launch_eta<T>(const DenseBufs<T> &, hipStream_t);                                       \
     template int dense_launch_gen_A<T>(T *, int, int, uint64_t, hipStream_t);                                  \

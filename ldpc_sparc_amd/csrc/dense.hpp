@@ -43,4 +43,8 @@ template <typename T>
 int glue_launch_llr(const T *beta, int B, int L, int M, int l0, int nl, double inv_sqrt_nPl, int llr_ld, T *llr,
                     int probs_only, hipStream_t s);
 
+template <typename T>
+int concat_launch_count(const int32_t *map_idx, const int32_t *true_idx, int B, int L, int L_unp, int logM,
+                        const T *app, const uint8_t *info, int mults, int N, int K, int64_t *counts, hipStream_t s);
+
 }  // namespace sg

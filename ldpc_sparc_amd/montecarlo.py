@@ -1,0 +1,190 @@
+"""Monte-Carlo error-rate campaigns sharded over GPUs.
+
+The reference parallelises only by launching independent processes with a
+`sim_id` (ldpc_jossy/py/ldpc_awgn.py:125-131, ldpc_jossy/README.md:144-148).
+Here one process per GPU runs a campaign together: every SNR point is split
+into fixed blocks of codewords, block b being seeded by (seed, point, b) so
+that the result does not depend on how many GPUs took part; each round the
+blocks are dealt to ranks by contiguous ranges, and ONE all-reduce of an int64
+counter vector (RCCL over xGMI between GPUs, or gloo for CPU tests) gives every
+rank the global counts that drive the stopping rule.
+
+Counters per point: [units, bit_errors, frame_errors, aux0, aux1] where aux
+is decoder-specific (BP: executed iterations; AMP: section errors, AMP
+iterations; concatenated: unprotected / protected bit errors).
+
+Checkpoint/resume: with `checkpoint_dir`, the global counters
+and next block of every point are written after each round; a restarted
+campaign continues from there.
+"""
+import json
+import os
+
+import numpy as np
+
+from . import _native
+
+NC = 5
+
+
+def shard_range(total, rank, world):
+    """[start, end) of rank's share of `total` items (contiguous, balanced)."""
+    return total * rank // world, total * (rank + 1) // world
+
+
+class Aggregator:
+    """Sum of int64 counter vectors over the ranks of a campaign."""
+
+    def __init__(self, backend="none", comm=None):
+        assert backend in ("none", "gloo", "rccl")
+        self.backend = backend
+        self.comm = comm
+        self._dbuf = None
+        if backend == "gloo":
+            import torch.distributed as dist
+            self.dist = dist
+
+    def allreduce(self, counts):
+        counts = np.ascontiguousarray(counts, dtype=np.int64)
+        if self.backend == "none":
+            return counts.copy()
+        if self.backend == "gloo":
+            import torch
+            t = torch.from_numpy(counts.copy())
+            self.dist.all_reduce(t)
+            return t.numpy().astype(np.int64)
+        if self._dbuf is None or self._dbuf.nbytes < counts.nbytes:
+            self._dbuf = _native.DeviceBuffer(counts.nbytes)
+        self._dbuf.upload(counts)
+        self.comm.allreduce_sum_i64(self._dbuf, counts.size)
+        _native.synchronize()
+        return self._dbuf.download(np.empty_like(counts))
+
+
+def _ckpt_path(checkpoint_dir, tag, point):
+    return os.path.join(checkpoint_dir, f"{tag}_pt{point}.json")
+
+
+def run_point(trial, point, *, block, blocks_per_round, rank, world, agg, min_errors=None, max_units=None,
+              checkpoint_dir=None, tag="campaign"):
+    """Run one point until `min_errors` frame errors or `max_units` units
+    (globally).  trial(point, first_block, n_blocks, block) -> int64[NC]
+    counters of the blocks [first_block, first_block + n_blocks)."""
+    total = np.zeros(NC, dtype=np.int64)
+    next_block = 0
+    if checkpoint_dir:
+        path = _ckpt_path(checkpoint_dir, tag, point)
+        if os.path.exists(path):
+            with open(path) as f:
+                st = json.load(f)
+            total = np.array(st["counts"], dtype=np.int64)
+            next_block = int(st["next_block"])
+    while True:
+        if min_errors is not None and total[2] >= min_errors:
+            break
+        if max_units is not None and total[0] >= max_units:
+            break
+        nb = blocks_per_round
+        if max_units is not None:
+            nb = min(nb, -(-(max_units - int(total[0])) // block))
+        a, b = shard_range(nb, rank, world)
+        local = trial(point, next_block + a, b - a, block) if b > a else np.zeros(NC, dtype=np.int64)
+        total = total + agg.allreduce(local)  # the campaign's one collective per round
+        next_block += nb
+        if checkpoint_dir and rank == 0:
+            os.makedirs(checkpoint_dir, exist_ok=True)
+            tmp = _ckpt_path(checkpoint_dir, tag, point) + ".tmp"
+            with open(tmp, "w") as f:
+                json.dump({"counts": total.tolist(), "next_block": next_block}, f)
+            os.replace(tmp, _ckpt_path(checkpoint_dir, tag, point))
+        if min_errors is None and max_units is None:
+            break
+    return total
+
+
+# ------------------------------------------------------------------ LDPC over BPSK/AWGN
+
+
+class LdpcTrial:
+    """Random codewords over BPSK/AWGN at Es/N0 = snr dB (ldpc_awgn.py:39-56),
+    decoded in batches on the GPU; counts over all N bits as the reference
+    does (ldpc_awgn.py:97-104).  aux0 = sum of decode iteration counts."""
+
+    def __init__(self, c, snrs, dectype="sumprod2", max_it=200, corr=0.7, precision="f32", seed=0):
+        self.c, self.snrs, self.dectype = c, list(snrs), dectype
+        self.max_it, self.corr, self.seed = int(max_it), float(corr), int(seed)
+        self.prec = {"f64": _native.SG_F64, "f32": _native.SG_F32}[precision]
+
+    def __call__(self, point, first_block, n_blocks, block):
+        c = self.c
+        sigma2 = 1.0 / np.power(10, self.snrs[point] / 10.0)
+        X, LLR = [], []
+        for blk in range(first_block, first_block + n_blocks):
+            rng = np.random.default_rng([self.seed, point, blk])
+            x = c.encode_batch(rng.integers(0, 2, (block, c.K)))
+            y = (1.0 - 2.0 * x) + np.sqrt(sigma2) * rng.standard_normal(x.shape)
+            X.append(x)
+            LLR.append(2.0 / sigma2 * y)
+        X = np.concatenate(X)
+        LLR = np.concatenate(LLR)
+        B = X.shape[0]
+        dt = np.float64 if self.prec == _native.SG_F64 else np.float32
+        lib = _native.lib()
+        g = c._device_graph()
+        d_ch = _native.DeviceBuffer.from_array(LLR.astype(dt))
+        d_app = _native.DeviceBuffer(B * c.N * np.dtype(dt).itemsize)
+        d_it = _native.DeviceBuffer(B * 4)
+        d_x = _native.DeviceBuffer.from_array(X.astype(np.uint8))
+        d_cnt = _native.DeviceBuffer(32)
+        d_cnt.zero()
+        _native.check(lib.sg_ldpc_decode_device(g, _native.DECTYPES[self.dectype], self.prec, d_ch.ptr, B,
+                                                self.max_it, self.corr, d_app.ptr, d_it.ptr, None))
+        _native.check(lib.sg_ldpc_count_errors_device(g, self.prec, d_app.ptr, d_x.ptr, d_it.ptr, B, c.K,
+                                                      d_cnt.ptr, None))
+        _native.synchronize()
+        cnt = d_cnt.download(np.zeros(4, np.int64))
+        return np.array([B, cnt[0], cnt[1], cnt[3], 0], dtype=np.int64)
+
+
+def ldpc_awgn_campaign(standard, rate, z, ptype="A", *, rank=0, world=1, agg=None, N_MEASUREMENTS=24,
+                       C_AWGN_OFFSET=1.0, P_STEP=100.0, MIN_ERRORS=100, MAX_BLOCKS=400000, block=256,
+                       blocks_per_round=16, dectype="sumprod2", max_it=200, precision="f32", seed=0,
+                       results_file=None, checkpoint_dir=None):
+    """The BER/FER campaign of ldpc_awgn.sim (ldpc_awgn.py:60-114) on the GPU(s):
+    same starting SNR, stopping rule and SNR-step heuristic; returns and (rank
+    0) appends the result tuples (standard, rate, z, ptype, SNR, nblocks,
+    nblockerrors, nblocks*K, nbiterrors, nit_total) -- the 11-field form that
+    results2csv.c parses (results2csv.c:47-48)."""
+    from .ldpc import code
+    Rv = {"1/2": .5, "2/3": 0.6667, "3/4": 0.75, "5/6": 0.83333}
+    if rate not in Rv:
+        raise NameError("Rate unsupported")
+    agg = agg or Aggregator()
+    c = code(standard, rate, z, ptype)
+    snr = 10.0 * np.log10(np.power(2, Rv[rate]) - 1.0) + C_AWGN_OFFSET
+    res = []
+    trial = LdpcTrial(c, [], dectype, max_it, 0.7, precision, seed)
+    for point in range(N_MEASUREMENTS):
+        trial.snrs.append(snr)
+        tot = run_point(trial, point, block=block, blocks_per_round=blocks_per_round, rank=rank, world=world,
+                        agg=agg, min_errors=MIN_ERRORS, max_units=MAX_BLOCKS, checkpoint_dir=checkpoint_dir,
+                        tag=f"ldpc_{standard}_{rate.replace('/', '')}_{z}_{ptype}")
+        nblocks = int(tot[0])
+        out = (standard, rate, z, ptype, snr, nblocks, int(tot[2]), nblocks * c.K, int(tot[1]), int(tot[3]))
+        res.append(out)
+        if results_file and rank == 0:
+            with open(results_file, "a") as f:
+                f.write(str(out) + "\n")
+        snr += np.sqrt(P_STEP / nblocks)
+    return res
+
+
+def results_to_csv(lines):
+    """The conversion of results2csv.c:47-72 (standard code, rate, type, z, SNR,
+    nblocks, nblockerrors, nbits, nbiterrors, nit) for result tuples."""
+    out = []
+    for (std, rate, z, ptype, snr, nb, nbe, nbits, nber, nit) in lines:
+        num, den = (int(v) for v in rate.split("/"))
+        out.append(f"{'16' if std[5] == '6' else '11'}, {num / den:g}, {0 if ptype == 'A' else 1}, {z}, "
+                   f"{snr:g}, {nb}, {nbe}, {nbits}, {nber}, {nit}")
+    return out
