@@ -54,6 +54,10 @@ def parse():
     ap.add_argument("--bp-ebn0", type=float, default=2.0)
     ap.add_argument("--bp-steps", type=int, default=10)
     ap.add_argument("--no-bp", action="store_true")
+    ap.add_argument("--no-concat", action="store_true")
+    ap.add_argument("--concat-batch", type=int, default=256)
+    ap.add_argument("--concat-steps", type=int, default=2)
+    ap.add_argument("--concat-ebn0", type=float, default=4.0)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="approximate CPU-baseline sample length (0 disables)")
     ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
@@ -211,6 +215,55 @@ def bp_cpu_baseline(st, seconds):
                       f"{st.get('ebn0')} dB) by oracle/bp_oracle.c on 1 host core"}
 
 
+# ------------------------------------------------------------------ concatenated (C5)
+
+MFMA_F32_PEAK_TFS = 157.3  # MI355X f32 MFMA dense peak (MI355X_MICROARCH.md)
+
+
+def concat_bench(args, d):
+    """C5: SPARC(L=1024, M=512, n=6144, dense Gaussian design shared by the
+    batch) + 4 x LDPC 802.11n r1/2 z=81, semi-protected (160 uncoded sections),
+    AMP 25 it -> glue -> sumprod2 BP 200 it, all on the device."""
+    from ldpc_sparc_amd.pipeline import ConcatPipeline
+    L, M, n, P, Lu, mults = 1024, 512, 6144, 15.0, 160, 4
+    pipe = ConcatPipeline(L, M, n, P, Lu, mults, design_seed=1234 + d.rank, precision="f32", t_max=25)
+    R_overall = (Lu * 9 + mults * pipe.c.K) / n
+    var = P / (2 * R_overall * 10 ** (args.concat_ebn0 / 10))
+    B = args.concat_batch
+    pipe.make_batch(B, var, np.random.default_rng(5000 + d.rank))
+    pipe.reset_counts()
+    pipe.decode()  # warmup
+    _native.device_synchronize()
+    pipe.reset_counts()
+    prof = _native.Profiler()
+    d.barrier()
+    _native.device_synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.concat_steps):
+        pipe.decode()
+    _native.device_synchronize()
+    el = d.max(time.perf_counter() - t0)
+    ph = prof.stop()
+    cnt = pipe.counts()
+    gemm_ms = ph.get("dense_gemm", (0.0, 0))[0]
+    flops = 4.0 * n * L * M * B * (2 * 25 - 1) / 2 * args.concat_steps  # 2 n LM B per product, 49 products
+    ach = flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms else None
+    user_bits = Lu * 9 + mults * pipe.c.K
+    return {"workload": "C5: SPARC(L=1024, M=512, n=6144, dense Gaussian design shared by the batch) + "
+                        "4 x LDPC 802.11n r1/2 z=81 semi-protected (160 uncoded sections); AMP 25 it, "
+                        "glue, sumprod2 BP 200 it",
+            "value": d.world * B * args.concat_steps / el, "unit": "codewords/s", "batch_per_gpu": B,
+            "ebn0_db": args.concat_ebn0, "awgn_var": var, "R_overall": R_overall,
+            "ber": float(cnt[1]) / (cnt[0] * user_bits) if cnt[0] else None,
+            "codeword_errors": int(cnt[2]), "codewords": int(cnt[0]),
+            "roofline": {"bound": "mfma", "achieved": ach, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
+                         "frac": ach / MFMA_F32_PEAK_TFS if ach else None, "traffic": None,
+                         "kernel": "gemm_f32_mfma (A beta split-K NT + A^T z NN, v_mfma_f32_32x32x2_f32)",
+                         "algorithmic_flops_per_batch_iteration": 4.0 * n * L * M * B,
+                         "kernel_ms": {k: round(v[0], 3) for k, v in ph.items()},
+                         "launches": {k: v[1] for k, v in ph.items()}}}
+
+
 def main():
     args = parse()
     d = Dist()
@@ -306,6 +359,9 @@ def main():
                                   "kernel": "bp_flood_kernel<float, minsum>",
                                   "algorithmic_bytes_per_codeword_iteration": bbytes,
                                   "kernel_ms": bp_ms, "launches": ph.get("bp_flood", (0, 0))[1]}}
+
+    if not args.no_concat:
+        out["concat"] = concat_bench(args, d)
 
     if d.rank == 0 and d.world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = amp_cpu_baseline(st, args, args.cpu_seconds)

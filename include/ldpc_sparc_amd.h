@@ -99,6 +99,10 @@ int sg_dense_amp_device(sg_dense_plan *p, const void *d_y, int B, int t_max, voi
  * y [n], beta [L*M], z [n], tau_sqr -> beta', z', tau_sqr'. */
 int sg_dense_amp_iteration(sg_dense_plan *p, const double *y, const double *beta, const double *z,
                            double tau_sqr, double *beta_out, double *z_out, double *tau_sqr_out);
+/* Device pointers of the plan's own beta and s [B][L*M] after the last
+ * sg_dense_amp_device call (valid until the next call; lets a pipeline feed
+ * the glue without copies). */
+int sg_dense_state_device(sg_dense_plan *p, void **d_beta, void **d_s);
 /* x = A beta0 for one-hot beta0 (section index d_idx [B][L], value sqrt(n P / L)). */
 int sg_dense_encode_device(sg_dense_plan *p, const int32_t *d_idx, int B, void *d_x, void *stream);
 /* MAP section indices of s [B][L*M] (msg_vector_map_estimator, sparc_new.py:1099-1116). */

@@ -333,6 +333,13 @@ int sg_dense_encode_device(sg_dense_plan *p, const int32_t *d_idx, int B, void *
     return SG_OK;
 }
 
+int sg_dense_state_device(sg_dense_plan *p, void **d_beta, void **d_s) {
+    SG_CHECK_ARG(p, "plan is NULL");
+    if (d_beta) *d_beta = p->ws_beta;
+    if (d_s) *d_s = p->ws_s;
+    return SG_OK;
+}
+
 int sg_dense_map_device(sg_dense_plan *p, const void *d_s, int B, int32_t *d_idx, void *stream) {
     SG_CHECK_ARG(p && d_s && d_idx, "null argument");
     if (B <= 0) return SG_OK;
