@@ -296,6 +296,11 @@ def main():
     bytes_per_cwit = 4 * (2 * st["L"] * st["M"] + 4 * st["n"])
     achieved = bytes_per_cwit * cw_it / (amp_ms * 1e-3) / 1e9 if amp_ms > 0 else None
     total_cw = d.world * st["B"] * args.steps
+    traffic = None
+    tpath = os.path.join(REPO, "profiles", "r01_pmc_traffic_amp_c2.json")
+    if os.path.exists(tpath):  # rocprofv3 --pmc passes of tools/pmc_traffic.py (same kernels, B=64)
+        with open(tpath) as f:
+            traffic = json.load(f)["hbm_bytes_per_codeword_iteration"]
     out = {
         "metric": METRIC,
         "value": total_cw / el_max,
@@ -316,7 +321,9 @@ def main():
                    "parallelism": f"mc-shard x{d.world} (independent codewords per GPU, "
                                   "RCCL all-reduce of error counters)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+                     "traffic_unit": "HBM bytes per codeword-iteration (PMC FETCH_SIZE*2 + WRITE_SIZE, "
+                                     "profiles/r01_pmc_traffic_amp_c2.json)",
                      "kernel": "one AMP iteration = " + "+".join(AMP_PHASES),
                      "algorithmic_bytes_per_codeword_iteration": bytes_per_cwit,
                      "codeword_iterations": cw_it,

@@ -81,7 +81,8 @@ __global__ __launch_bounds__(1024) void reg_ab_stage1(RegTables<T> tb, RegBufs<T
     const int m2 = blockIdx.x, t = blockIdx.y, cw = blockIdx.z;
     if (bf.mode == 0 && !bf.active[cw] && !tb.skip) return;
     const int tid = threadIdx.x, nthr = blockDim.x;
-    for (int i = tid; i < 2 * Pp; i += nthr) dr[i] = T(0);
+    if (!(tb.skip & 16))
+        for (int i = tid; i < 2 * Pp; i += nthr) dr[i] = T(0);
     for (int i = tid; i < 64 + tb.nB; i += nthr)
         ta[i] = i < 64 ? tb.twa[m2 * 64 + i] : tb.twb[m2 * tb.nB + i - 64];
     const size_t tc = (size_t)t * tb.Mc;
@@ -291,7 +292,8 @@ __global__ __launch_bounds__(1024) void reg_az_stage2(RegTables<T> tb, RegBufs<T
     const int m2 = blockIdx.x, t = blockIdx.y, cw = blockIdx.z;
     if (bf.mode == 0 && !bf.active[cw] && !tb.skip) return;
     const int tid = threadIdx.x, nthr = blockDim.x;
-    for (int i = tid; i < 2 * Pp; i += nthr) dr[i] = T(0);
+    if (!(tb.skip & 16))
+        for (int i = tid; i < 2 * Pp; i += nthr) dr[i] = T(0);
     T tp = T(1), inv_tp = T(1);
     const bool have_beta = bf.mode == 0 && t_iter > 0;
     if (have_beta) {  // beta of the previous iteration = softmax(s_prev) with tau_prev
@@ -381,7 +383,7 @@ __global__ __launch_bounds__(1024) void reg_az_stage2(RegTables<T> tb, RegBufs<T
     // one thread per section over its contiguous segment (segments average
     // ~16 entries: the fpad skew spreads the threads over the LDS banks)
     constexpr int RC = 16;  // LDS reads in flight per thread
-    for (int l = tid; l < tb.Lblk; l += nthr) {
+    for (int l = tid; l < ((tb.skip & 8) ? 0 : tb.Lblk); l += nthr) {
         const int a = sg[l], b = sg[l + 1];
         T m = -INFINITY;
         for (int c = a; c < b; c += RC) {

@@ -43,3 +43,8 @@ for r in range(reps):
     cnt = d_cnt.download(np.zeros(4, np.int64))
     print(f"rep {r}: {dt*1e3:.1f} ms  {B/dt:.1f} cw/s  sec_err={cnt[0]} bit_err={cnt[1]} "
           f"cw_err={cnt[2]} iters={cnt[3]/B:.2f}", flush=True)
+    total_cwit = total_cwit + int(cnt[3]) if r else int(cnt[3])
+if len(sys.argv) > 4:
+    import json
+    with open(sys.argv[4], "w") as f:
+        json.dump({"B": B, "reps": reps, "codeword_iterations": total_cwit}, f)
