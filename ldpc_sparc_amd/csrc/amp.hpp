@@ -98,6 +98,8 @@ struct RegTables {
     const cx<T> *stw;         // per-stage P-point FFT twiddles (lds_fft1)
     const cx<T> *twa, *twb;   // w_N2^(m2 k1) = twa[m2][k1 & 63] * twb[m2][k1 >> 6]
     int nB;                   // ceil(P / 64)
+    int ept;                  // stage-1 FFT elements per thread (block = P / ept)
+    int maxcls;               // largest class (entries of one m2 within a column block)
     int skip;                 // timing ablation only (SG_AMP_SKIP): 1 FFT, 2 gather/scatter, 4 row I/O
 };
 
@@ -135,7 +137,12 @@ int reg_launch_map(const RegTables<T> &tb, const RegBufs<T> &bf, hipStream_t s);
 template <typename T>
 int reg_launch_ab_finish(const RegTables<T> &tb, const RegBufs<T> &bf, hipStream_t s);
 size_t reg_stage1_lds(int P, int Lblk, size_t real_bytes);
-inline int reg_ept(int P) { return P / 1024 > 8 ? P / 1024 : 8; }  // stage-1 elements per thread
+// stage-1 elements per thread: f32 at P >= 8192 uses 16 (P = 8192 -> 512-thread
+// workgroups, two per CU); otherwise P/1024 threads' worth, at least 8
+inline int reg_ept(int P, size_t real_bytes) {
+    if (real_bytes == 4 && P >= 8192) return 16;
+    return P / 1024 > 8 ? P / 1024 : 8;
+}
 int reg_launch_init(int B, int Lc, int t_max, double *nmse, int32_t *active, int32_t *t_final, hipStream_t s);
 
 template <typename T>

@@ -43,6 +43,13 @@ __device__ __forceinline__ float sm_arg<float>(float v, float m, float, float in
 template <>
 __device__ __forceinline__ double sm_arg<double>(double v, double m, double tau, double) { return v / tau - m / tau; }
 
+// Section statistics of the single-precision engine are kept as sums over
+// every entry but the maximum (whose term is exactly 1), so 1 - sum beta^2
+// and the NMSE of decoded sections, ~1e-7 and below, come without the
+// cancellation of 1 - S2/S1^2 in float.  Double keeps the reference's sums.
+template <typename T>
+inline constexpr bool kRestSums = sizeof(T) == 4;
+
 // w_N2^(m2 k1), m2 < Q, k1 < P, from two small tables (contiguous per m2)
 template <typename T>
 __device__ __forceinline__ cx<T> reg_tw2(const RegTables<T> &tb, int m2, int k1) {
@@ -62,6 +69,9 @@ __device__ __forceinline__ double reg_block_sum(double v, double *red) {
 
 constexpr int REG_CH = 8;  // entries a thread loads before using them
 
+// block size of a stage-1 kernel: P / EPT for the compile-time sizes
+constexpr int reg_s1_threads(int EPT, int LOG2P) { return LOG2P > 0 ? (1 << LOG2P) / EPT : 1024; }
+
 size_t reg_stage1_lds(int P, int Lblk, size_t real_bytes) {
     return (size_t)(P + (P >> 4)) * 2 * real_bytes + (size_t)2 * Lblk * real_bytes +
            (size_t)(64 + (P + 63) / 64) * 2 * real_bytes;
@@ -69,11 +79,11 @@ size_t reg_stage1_lds(int P, int Lblk, size_t real_bytes) {
 
 // ------------------------------------------------------------------ ab stage 1
 template <typename T, int EPT, int LOG2P>
-__global__ __launch_bounds__(1024) void reg_ab_stage1(RegTables<T> tb, RegBufs<T> bf) {
+__global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_ab_stage1(RegTables<T> tb, RegBufs<T> bf) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     cx<T> *d = reinterpret_cast<cx<T> *>(smem);
     T *dr = reinterpret_cast<T *>(smem);
-    const int Pp = tb.P + (tb.P >> 4);  // padded FFT array (fpad)
+    const int Pp = tb.P + (tb.P >> 4);  // FFT image (fsw) and the skewed class image (fpad)
     T *sM = dr + 2 * (size_t)Pp;
     T *sI = sM + tb.Lblk;
     cx<T> *ta = reinterpret_cast<cx<T> *>(sI + tb.Lblk);  // w_N2^(m2 k1) factors of this class
@@ -82,7 +92,7 @@ __global__ __launch_bounds__(1024) void reg_ab_stage1(RegTables<T> tb, RegBufs<T
     if (bf.mode == 0 && !bf.active[cw] && !tb.skip) return;
     const int tid = threadIdx.x, nthr = blockDim.x;
     if (!(tb.skip & 16))
-        for (int i = tid; i < 2 * Pp; i += nthr) dr[i] = T(0);
+        for (int i = tid; i < tb.P * (int)sizeof(cx<T>) / 16; i += nthr) reinterpret_cast<uint4 *>(smem)[i] = uint4{0, 0, 0, 0};
     for (int i = tid; i < 64 + tb.nB; i += nthr)
         ta[i] = i < 64 ? tb.twa[m2 * 64 + i] : tb.twb[m2 * tb.nB + i - 64];
     const size_t tc = (size_t)t * tb.Mc;
@@ -144,7 +154,7 @@ __global__ __launch_bounds__(1024) void reg_ab_stage1(RegTables<T> tb, RegBufs<T
 #pragma unroll
     for (int i = 0; i < EPT; ++i) {
         const int r = tid + i * nthr;
-        if (r < nR) out[r] = cmul(d[fpad(k1[i])], cmul(ta[k1[i] & 63], tbb[k1[i] >> 6]));
+        if (r < nR) out[r] = cmul(d[fsw(k1[i])], cmul(ta[k1[i] & 63], tbb[k1[i] >> 6]));
     }
 }
 
@@ -163,23 +173,22 @@ __global__ __launch_bounds__(256) void reg_ab_stage2(RegTables<T> tb, RegBufs<T>
     const int tid = threadIdx.x, nthr = blockDim.x;
     for (int i = tid; i < tb.Q; i += nthr) twq[i] = tb.twQ[i];
     const cx<T> *src = bf.tu + ((size_t)cw * tb.nT + t) * tb.Q * tb.nRmax;
-    // rows [r0, r1) of every m2 plane; REG_CH loads in flight per thread
-    for (int base = tid; base < tb.Q * nr; base += REG_CH * nthr) {
-        cx<T> v[REG_CH];
+    // rows [r0, r1) of every m2 plane: thread -> (row rr, planes m2 = m2a +
+    // j * mstep), REG_CH loads in flight (RB divides the block size)
+    const int rr = tid % tb.RB, mstep = nthr / tb.RB;
+    if (rr < nr) {
+        const cx<T> *sp = src + r0 + rr;
+        for (int m0 = tid / tb.RB; m0 < tb.Q; m0 += REG_CH * mstep) {
+            cx<T> v[REG_CH];
 #pragma unroll
-        for (int i = 0; i < REG_CH; ++i) {
-            const int e = base + i * nthr;
-            if (e < tb.Q * nr) {
-                const int m2 = e / nr, r = e - m2 * nr;
-                v[i] = src[(size_t)m2 * tb.nRmax + r0 + r];
+            for (int i = 0; i < REG_CH; ++i) {
+                const int m2 = m0 + i * mstep;
+                if (m2 < tb.Q) v[i] = sp[(size_t)m2 * tb.nRmax];
             }
-        }
 #pragma unroll
-        for (int i = 0; i < REG_CH; ++i) {
-            const int e = base + i * nthr;
-            if (e < tb.Q * nr) {
-                const int m2 = e / nr, r = e - m2 * nr;
-                d[m2 * tb.RB + r] = v[i];
+            for (int i = 0; i < REG_CH; ++i) {
+                const int m2 = m0 + i * mstep;
+                if (m2 < tb.Q) d[m2 * tb.RB + rr] = v[i];
             }
         }
     }
@@ -267,33 +276,35 @@ __global__ __launch_bounds__(256) void reg_az_stage1(RegTables<T> tb, RegBufs<T>
     __syncthreads();
     cx<T> *dst = bf.tu + ((size_t)cw * tb.nT + t) * tb.Q * tb.nRmax;
     const int qm = tb.Q - 1;
-    for (int e = tid; e < tb.Q * nr; e += nthr) {
-        const int m2 = e / nr, r = e - m2 * nr;
-        const int a = rkp[r], b = rkp[r + 1];
-        cx<T> acc{T(0), T(0)};
-        for (int k = a; k < b; ++k) {
-            const cx<T> v = g[k], w = twq[(m2 * rk2[k]) & qm];  // v * conj(w)
-            acc.x += v.x * w.x + v.y * w.y;
-            acc.y += v.y * w.x - v.x * w.y;
+    const int rr = tid % tb.RB, mstep = nthr / tb.RB;  // thread -> (row rr, planes m2a + j mstep)
+    if (rr < nr) {
+        const int a = rkp[rr], b = rkp[rr + 1], k1 = rk1[rr];
+        for (int m2 = tid / tb.RB; m2 < tb.Q; m2 += mstep) {
+            cx<T> acc{T(0), T(0)};
+            for (int k = a; k < b; ++k) {
+                const cx<T> v = g[k], w = twq[(m2 * rk2[k]) & qm];  // v * conj(w)
+                acc.x += v.x * w.x + v.y * w.y;
+                acc.y += v.y * w.x - v.x * w.y;
+            }
+            dst[(size_t)m2 * tb.nRmax + r0 + rr] = cmul(acc, cconj(reg_tw2(tb, m2, k1)));
         }
-        dst[(size_t)m2 * tb.nRmax + r0 + r] = cmul(acc, cconj(reg_tw2(tb, m2, rk1[r])));
     }
 }
 
 // ------------------------------------------------------------------ az stage 2
 template <typename T, int EPT, int LOG2P>
-__global__ __launch_bounds__(1024) void reg_az_stage2(RegTables<T> tb, RegBufs<T> bf, int t_iter) {
+__global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_az_stage2(RegTables<T> tb, RegBufs<T> bf, int t_iter) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     cx<T> *d = reinterpret_cast<cx<T> *>(smem);
     T *dr = reinterpret_cast<T *>(smem);
-    const int Pp = tb.P + (tb.P >> 4);  // padded FFT array (fpad)
+    const int Pp = tb.P + (tb.P >> 4);  // FFT image (fsw) and the skewed class image (fpad)
     T *sM = dr + 2 * (size_t)Pp;
     T *sI = sM + tb.Lblk;
     const int m2 = blockIdx.x, t = blockIdx.y, cw = blockIdx.z;
     if (bf.mode == 0 && !bf.active[cw] && !tb.skip) return;
     const int tid = threadIdx.x, nthr = blockDim.x;
     if (!(tb.skip & 16))
-        for (int i = tid; i < 2 * Pp; i += nthr) dr[i] = T(0);
+        for (int i = tid; i < tb.P * (int)sizeof(cx<T>) / 16; i += nthr) reinterpret_cast<uint4 *>(smem)[i] = uint4{0, 0, 0, 0};
     T tp = T(1), inv_tp = T(1);
     const bool have_beta = bf.mode == 0 && t_iter > 0;
     if (have_beta) {  // beta of the previous iteration = softmax(s_prev) with tau_prev
@@ -323,7 +334,7 @@ __global__ __launch_bounds__(1024) void reg_az_stage2(RegTables<T> tb, RegBufs<T
         }
 #pragma unroll
         for (int i = 0; i < REG_CH; ++i)
-            if (base + i * nthr < nR) d[fpad(k1[i])] = v[i];
+            if (base + i * nthr < nR) d[fsw(k1[i])] = v[i];
     }
     __syncthreads();
     if (!(tb.skip & 1)) {
@@ -397,6 +408,7 @@ __global__ __launch_bounds__(1024) void reg_az_stage2(RegTables<T> tb, RegBufs<T
             for (int i = 0; i < RC; ++i) m = fmax(m, v[i]);
         }
         T S1 = T(0), S2 = T(0);
+        bool seen = !kRestSums<T>;  // f32: sums over the segment without its (first) maximum
         for (int c = a; c < b; c += RC) {
             T v[RC];
 #pragma unroll
@@ -404,7 +416,11 @@ __global__ __launch_bounds__(1024) void reg_az_stage2(RegTables<T> tb, RegBufs<T
 #pragma unroll
             for (int i = 0; i < RC; ++i)
                 if (c + i < b) {
-                    const T e = rexp<T>(sm_arg<T>(v[i], m, tau, inv_tau));
+                    T e = rexp<T>(sm_arg<T>(v[i], m, tau, inv_tau));
+                    if (!seen && v[i] == m) {
+                        seen = true;
+                        e = T(0);
+                    }
                     S1 += e;
                     S2 += e * e;
                 }
@@ -493,41 +509,84 @@ __global__ __launch_bounds__(1024) void reg_merge(RegTables<T> tb, RegBufs<T> bf
         const T *s = bf.s + (size_t)cw * tb.LM + (size_t)c * tb.Mc;
         double a = 0.0, e = 0.0;
         for (int ll = tid; ll < Lb; ll += nthr) {
-            T M = -INFINITY;
-            for (int m2 = 0; m2 < tb.Q; ++m2) {
-                const T *p = pm + (size_t)m2 * 3 * Lb;
-                if (p[Lb + ll] > T(0)) M = fmax(M, p[ll]);
-            }
-            T S1 = T(0), S2 = T(0);
-            for (int m2 = 0; m2 < tb.Q; ++m2) {
-                const T *p = pm + (size_t)m2 * 3 * Lb;
-                const T S = p[Lb + ll];
-                if (S > T(0)) {
-                    const T f = rexp<T>(sm_arg<T>(p[ll], M, tau, inv_tau));
-                    S1 += S * f;
-                    S2 += p[2 * Lb + ll] * (f * f);
-                }
-            }
             const int l = c * Lb + ll;
-            const T inv = T(1) / S1;
-            bf.stM[(size_t)cw * tb.L + l] = M;
-            bf.stI[(size_t)cw * tb.L + l] = inv;
-            const double ss = (double)(S2 * inv * inv);
-            double err = ss;
-            if (bf.true_idx) {
-                const int jl = ll * tb.M + bf.true_idx[(size_t)cw * tb.L + l];
-                const int q = tb.qpos[(size_t)c * tb.Mc + jl];
-                const double bt = (double)(rexp<T>(sm_arg<T>(s[q], M, tau, inv_tau)) * inv);
-                err = ss - 2.0 * bt + 1.0;
+            int jt = -1;
+            if (bf.true_idx) jt = tb.qpos[(size_t)c * tb.Mc + ll * tb.M + bf.true_idx[(size_t)cw * tb.L + l]];
+            if constexpr (kRestSums<T>) {
+                // partials hold (max, sums without the max); the section's
+                // designated maximum is the first partial attaining M
+                T M = -INFINITY;
+                int pmx = -1;
+                for (int m2 = 0; m2 < tb.Q; ++m2) {
+                    const T mv = pm[(size_t)m2 * 3 * Lb + ll];
+                    if (mv > M) {
+                        M = mv;
+                        pmx = m2;
+                    }
+                }
+                T R1 = T(0), R2 = T(0);
+                for (int m2 = 0; m2 < tb.Q; ++m2) {
+                    const T *p = pm + (size_t)m2 * 3 * Lb;
+                    if (!(p[ll] > -INFINITY)) continue;  // empty segment
+                    if (m2 == pmx) {
+                        R1 += p[Lb + ll];
+                        R2 += p[2 * Lb + ll];
+                    } else {
+                        const T f = rexp<T>(sm_arg<T>(p[ll], M, tau, inv_tau));
+                        R1 += (T(1) + p[Lb + ll]) * f;
+                        R2 += (T(1) + p[2 * Lb + ll]) * (f * f);
+                    }
+                }
+                const T inv = T(1) / (T(1) + R1);
+                bf.stM[(size_t)cw * tb.L + l] = M;
+                bf.stI[(size_t)cw * tb.L + l] = inv;
+                // 1 - sum beta^2 = (2 R1 + R1^2 - R2) / (1 + R1)^2, no cancellation
+                const double i2 = (double)inv * (double)inv, r1 = R1, r2 = R2;
+                a += (2.0 * r1 + r1 * r1 - r2) * i2;
+                if (jt >= 0) {
+                    const T st = s[jt];
+                    if (st == M)  // the true entry is a maximum: |beta - beta0|^2 = R1^2 + R2 over (1 + R1)^2
+                        e += (r1 * r1 + r2) * i2;
+                    else {
+                        const double bt = (double)(rexp<T>(sm_arg<T>(st, M, tau, inv_tau)) * inv);
+                        e += (1.0 + r2) * i2 - 2.0 * bt + 1.0;
+                    }
+                }
+            } else {
+                T M = -INFINITY;
+                for (int m2 = 0; m2 < tb.Q; ++m2) {
+                    const T *p = pm + (size_t)m2 * 3 * Lb;
+                    if (p[Lb + ll] > T(0)) M = fmax(M, p[ll]);
+                }
+                T S1 = T(0), S2 = T(0);
+                for (int m2 = 0; m2 < tb.Q; ++m2) {
+                    const T *p = pm + (size_t)m2 * 3 * Lb;
+                    const T S = p[Lb + ll];
+                    if (S > T(0)) {
+                        const T f = rexp<T>(sm_arg<T>(p[ll], M, tau, inv_tau));
+                        S1 += S * f;
+                        S2 += p[2 * Lb + ll] * (f * f);
+                    }
+                }
+                const T inv = T(1) / S1;
+                bf.stM[(size_t)cw * tb.L + l] = M;
+                bf.stI[(size_t)cw * tb.L + l] = inv;
+                const double ss = (double)(S2 * inv * inv);
+                double err = ss;
+                if (jt >= 0) {
+                    const double bt = (double)(rexp<T>(sm_arg<T>(s[jt], M, tau, inv_tau)) * inv);
+                    err = ss - 2.0 * bt + 1.0;
+                }
+                a += ss;
+                e += err;
             }
-            a += ss;
-            e += err;
         }
         a = reg_block_sum(a, red);
         e = reg_block_sum(e, red);
         if (tid == 0) {
             const double denom = (Lc == 1) ? (double)tb.L : (double)Lb;
-            psi[c] = 1.0 - a / denom;
+            // f32 accumulates 1 - sum beta^2 per section; f64 the reference's sum beta^2
+            psi[c] = kRestSums<T> ? a / denom : 1.0 - a / denom;
             nmse[(size_t)(t + 1) * Lc + c] = e / denom;
         }
     }
@@ -596,7 +655,8 @@ static void launch_s2i(const RegTables<T> &tb, const RegBufs<T> &bf, int t_iter,
     hipLaunchKernelGGL((reg_az_stage2<T, EPT, LOG2P>), dim3(tb.Q, tb.nT, bf.B), dim3(tb.P / EPT), lds, s, tb, bf,
                        t_iter);
 }
-// compile-time FFT for the benchmark sizes (f32: P = 2^14; f64: P = 2^13)
+// compile-time FFT for the benchmark sizes (f32: P = 2^14 at EPT 16; f64:
+// P = 2^13 at EPT 8)
 constexpr int reg_hot_log2p(bool dbl) { return dbl ? 13 : 14; }
 
 template <typename T>
@@ -620,7 +680,7 @@ int reg_launch_ab(const RegTables<T> &tb, const RegBufs<T> &bf, hipStream_t s) {
     if (bf.B <= 0) return SG_OK;
     SG_TRY(reg_set_attrs<T>());
     const size_t lds1 = reg_stage1_lds(tb.P, tb.Lblk, sizeof(T));
-    const int ept = reg_ept(tb.P);
+    const int ept = tb.ept;
     {
         ProfScope ps(SG_PH_AB_A, s);
         constexpr int H = reg_hot_log2p(sizeof(T) == 8), HE = sizeof(T) == 8 ? 8 : 16;
@@ -658,7 +718,7 @@ int reg_launch_az(const RegTables<T> &tb, const RegBufs<T> &bf, int t_iter, hipS
     }
     SG_HIP(hipGetLastError());
     const size_t lds1 = reg_stage1_lds(tb.P, tb.Lblk, sizeof(T));
-    const int ept = reg_ept(tb.P);
+    const int ept = tb.ept;
     {
         ProfScope ps(SG_PH_AZ_B, s);
         constexpr int H = reg_hot_log2p(sizeof(T) == 8), HE = sizeof(T) == 8 ? 8 : 16;

@@ -37,7 +37,7 @@ struct sg_amp_plan {
     int32_t *ws_active = nullptr, *ws_argmax = nullptr, *ws_true = nullptr, *ws_tfinal = nullptr;
     // regular engine (one transform per column block, amp_fused.hip)
     bool regular = false;
-    int rP = 0, rQ = 0, rlog2P = 0, nRmax = 0, nKmax = 0, RB = 0, nrb = 0, maxKb = 0, Lblk = 0, nB = 0;
+    int rP = 0, rQ = 0, rlog2P = 0, rept = 0, rmaxcls = 0, nRmax = 0, nKmax = 0, RB = 0, nrb = 0, maxKb = 0, Lblk = 0, nB = 0;
     int32_t *r_nR = nullptr, *r_row_k1 = nullptr, *r_kptr = nullptr, *r_kk2 = nullptr, *r_krho = nullptr;
     int32_t *r_oa = nullptr, *r_ob = nullptr, *r_gi = nullptr, *r_cls_ptr = nullptr, *r_cls_j = nullptr,
             *r_qpos = nullptr;
@@ -229,13 +229,17 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
     const int Lblk = p->L / p->Lc;
     SG_CHECK_ARG(Lblk < 65536, "too many sections per column block (%d)", Lblk);
     const size_t rb = p->precision == SG_F64 ? 8 : 4;
-    int P = (int)std::min<long long>(N2, p->precision == SG_F64 ? 8192 : 16384);
+    long long Pmax = p->precision == SG_F64 ? 8192 : 16384;
+    if (const char *e = getenv("SG_AMP_PMAX")) Pmax = std::max(8LL, std::min(Pmax, atoll(e)));  // tuning knob
+    int P = (int)std::min<long long>(N2, Pmax);
     while (P > 8 && reg_stage1_lds(P, Lblk, rb) > 160 * 1024) P >>= 1;
     SG_CHECK_ARG(reg_stage1_lds(P, Lblk, rb) <= 160 * 1024, "section statistics exceed the LDS budget");
     const int Q = (int)(N2 / P);
     p->rP = P; p->rQ = Q; p->rlog2P = ilog2(P); p->Lblk = Lblk;
+    p->rept = reg_ept(P, rb);
     const size_t cxb = 2 * rb;
     p->RB = (int)std::min<size_t>(128, std::max<size_t>(1, 32768 / ((size_t)Q * cxb)));
+    SG_CHECK_ARG(256 % p->RB == 0, "row block %d must divide 256", p->RB);
 
     std::vector<std::vector<int32_t>> row_k1(nT), kptr(nT), kk2(nT), krho(nT), oa(nT), ob(nT), gi(nT);
     std::vector<std::vector<cd>> oc(nT), gc(nT);
@@ -257,7 +261,7 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
             used[sl] = 1;
             const long long m = sl >> 1;
             m2of[j] = (int)(m % Q);
-            locof[j] = (int)(2 * fpad((int)(m / Q)) + (sl & 1));  // padded LDS layout of lds_fft1
+            locof[j] = (int)(2 * fsw((int)(m / Q)) + (sl & 1));  // swizzled LDS layout of lds_fft1
             cnt[m2of[j] + 1]++;
         }
         int32_t *cpt = cls_ptr.data() + (size_t)t * (Q + 1);
@@ -377,13 +381,13 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
     std::vector<cd> stw;
     {
         int radix[8];
-        const int ns = fft1_plan(p->rlog2P, reg_ept(P), radix);
+        const int ns = fft1_plan(p->rlog2P, p->rept, radix);
         int lns = 0;
         for (int st = 0; st < ns; ++st) {
             const int R = radix[st];
             const long long Ns = 1LL << lns;
-            for (long long k = 0; k < Ns; ++k)
-                for (int r = 1; r < R; ++r) stw.push_back(tw(r * k, Ns * R));
+            for (long long k = 0; k < Ns; ++k)  // fft.hpp tw_per_k / tw_exp layout
+                for (int q = 0; q < tw_per_k(R); ++q) stw.push_back(tw(tw_exp(R, q) * k, Ns * R));
             lns += ilog2(R);
         }
         if (stw.empty()) stw.push_back(cd(1, 0));
@@ -405,6 +409,9 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
     SG_TRY(upload_cx(p, &p->r_oc, f_oc));
     SG_TRY(upload(p, &p->r_gi, f_gi));
     SG_TRY(upload_cx(p, &p->r_gc, f_gc));
+    for (int t = 0; t < nT; ++t)
+        for (int m2 = 0; m2 < Q; ++m2)
+            p->rmaxcls = std::max(p->rmaxcls, cls_ptr[(size_t)t * (Q + 1) + m2 + 1] - cls_ptr[(size_t)t * (Q + 1) + m2]);
     SG_TRY(upload(p, &p->r_cls_ptr, cls_ptr));
     SG_TRY(upload(p, &p->r_cls_ls, cls_ls));
     SG_TRY(upload(p, &p->r_cls_j, cls_j));
@@ -422,7 +429,7 @@ template <typename T>
 static RegTables<T> rtables(const sg_amp_plan *p) {
     RegTables<T> tb;
     tb.nT = p->nT; tb.L = p->L; tb.M = p->M; tb.LM = p->LM; tb.n = p->n; tb.Lc = p->Lc; tb.Mc = p->Mc;
-    tb.Lblk = p->Lblk; tb.N2 = p->N2; tb.P = p->rP; tb.Q = p->rQ; tb.log2P = p->rlog2P;
+    tb.Lblk = p->Lblk; tb.N2 = p->N2; tb.P = p->rP; tb.Q = p->rQ; tb.log2P = p->rlog2P; tb.ept = p->rept; tb.maxcls = p->rmaxcls;
     tb.nRmax = p->nRmax; tb.nKmax = p->nKmax; tb.RB = p->RB; tb.nrb = p->nrb; tb.maxKb = p->maxKb;
     tb.nR = p->r_nR; tb.row_k1 = p->r_row_k1; tb.kptr = p->r_kptr; tb.kk2 = p->r_kk2; tb.krho = p->r_krho;
     tb.oa = p->r_oa; tb.ob = p->r_ob; tb.oc = (const cx<T> *)p->r_oc; tb.gi = p->r_gi; tb.gc = (const cx<T> *)p->r_gc;

@@ -197,9 +197,61 @@ __device__ void lds_fft(cx<T> *d, int log2n, int nseq, int es, int ss, const cx<
 // Twiddles come from a per-stage table laid out in thread order:
 // stw[k * (R - 1) + r - 1] = w_{Ns R}^{r k} (forward), so the R - 1 twiddles of
 // a butterfly are contiguous and a wavefront reads a contiguous range.
-// LDS layout of the single-sequence FFT: element i at fpad(i) = i + i/16,
-// which makes the power-of-two strides of the Stockham stores conflict-free.
+// LDS layout of the single-sequence FFT: element i at fsw(i), the low four
+// index bits XOR-swizzled by the next four.  Runs of 32 consecutive elements
+// (every stage's loads, and the stores of the later stages) stay inside one
+// aligned 32-element block, so a ds_read_b64 lane group touches 64 distinct
+// banks; the stride-16 stores of the first radix-16 stage land on 16 distinct
+// bank pairs.  Adding a multiple of 256 commutes with the swizzle.
+__host__ __device__ __forceinline__ int fsw(int i) { return i ^ ((i >> 4) & 15); }
+// Skewed layout of the class-ordered s image (reduction of section segments):
+// element i at fpad(i) = i + i/16, so one-thread-per-segment reads spread
+// over the banks.
 __host__ __device__ __forceinline__ int fpad(int i) { return i + (i >> 4); }
+
+// Stage twiddles w^(r k), r < R, of butterfly k are rebuilt from TWN(R) table
+// entries per k (a twentieth of the table traffic of R - 1 entries, and few
+// enough registers to be loaded a stage ahead):
+//   R = 16: w, w^2, w^3, w^4, w^8, w^12 -> w^(4a+b) = w^(4a) w^b (one product)
+//   R = 8:  w, w^2, w^3, w^4             -> w^(4+b) = w^4 w^b
+//   R = 4:  w -> w^2 = w w, w^3 = w w^2;  R = 2: w
+__host__ __device__ constexpr int tw_per_k(int R) { return R == 16 ? 6 : R == 8 ? 4 : 1; }
+// table exponents of the TWN(R) entries
+__host__ __device__ inline int tw_exp(int R, int t) {
+    if (R == 16) return t < 4 ? t + 1 : 4 * (t - 2);  // 1 2 3 4 8 12
+    return t + 1;                                     // R = 8: 1 2 3 4; R <= 4: 1
+}
+
+template <typename T, bool INV, int R>
+__device__ __forceinline__ void tw_expand(const cx<T> *wl, cx<T> *w /* [R], w[0] unused */) {
+    cx<T> a[tw_per_k(R)];
+#pragma unroll
+    for (int t = 0; t < tw_per_k(R); ++t) a[t] = INV ? cconj(wl[t]) : wl[t];
+    if constexpr (R == 2) {
+        w[1] = a[0];
+    } else if constexpr (R == 4) {
+        w[1] = a[0];
+        w[2] = cmul(a[0], a[0]);
+        w[3] = cmul(a[0], w[2]);
+    } else if constexpr (R == 8) {
+#pragma unroll
+        for (int b = 1; b < 4; ++b) {
+            w[b] = a[b - 1];
+            w[4 + b] = cmul(a[3], a[b - 1]);
+        }
+        w[4] = a[3];
+    } else {
+#pragma unroll
+        for (int b = 1; b < 4; ++b) w[b] = a[b - 1];
+        w[4] = a[3];
+        w[8] = a[4];
+        w[12] = a[5];
+#pragma unroll
+        for (int q = 1; q < 4; ++q)
+#pragma unroll
+            for (int b = 1; b < 4; ++b) w[4 * q + b] = cmul(w[4 * q], a[b - 1]);
+    }
+}
 
 template <typename T, bool INV, int R, int EPT>
 __device__ __forceinline__ void stockham1_stage(cx<T> *d, int log2n, int log2Ns, const cx<T> *__restrict__ stw,
@@ -215,16 +267,15 @@ __device__ __forceinline__ void stockham1_stage(cx<T> *d, int log2n, int log2Ns,
         const int j = tid + i * nthr;
         const int k = j & (Ns - 1);
 #pragma unroll
-        for (int r = 0; r < R; ++r) v[i * R + r] = d[fpad(j + r * nbf)];
+        for (int r = 0; r < R; ++r) v[i * R + r] = d[fsw(j + r * nbf)];
         if (log2Ns > 0) {
-            cx<T> w[R];
+            constexpr int TWN = tw_per_k(R);
+            cx<T> wl[TWN], w[R];
 #pragma unroll
-            for (int r = 1; r < R; ++r) w[r] = stw[k * (R - 1) + r - 1];
+            for (int t = 0; t < TWN; ++t) wl[t] = stw[k * TWN + t];
+            tw_expand<T, INV, R>(wl, w);
 #pragma unroll
-            for (int r = 1; r < R; ++r) {
-                if (INV) w[r].y = -w[r].y;
-                v[i * R + r] = cmul(v[i * R + r], w[r]);
-            }
+            for (int r = 1; r < R; ++r) v[i * R + r] = cmul(v[i * R + r], w[r]);
         }
         dftR<T, INV, R>(&v[i * R]);
         base_out[i] = ((j - k) << LR) + k;
@@ -233,7 +284,7 @@ __device__ __forceinline__ void stockham1_stage(cx<T> *d, int log2n, int log2Ns,
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) d[fpad(base_out[i] + r * Ns)] = v[i * R + r];
+        for (int r = 0; r < R; ++r) d[fsw(base_out[i] + r * Ns)] = v[i * R + r];
     }
     __syncthreads();
 }
@@ -245,10 +296,10 @@ __device__ __forceinline__ void stockham1_stage(cx<T> *d, int log2n, int log2Ns,
 // with radix-4 (or one radix-2) first.  Returns the number of stages.
 __host__ __device__ inline int fft1_plan(int log2n, int ept, int *radix /* [8] */) {
     int ns = 0;
-    if (ept >= 16) {
+    if (ept >= 16) {  // radix-16 stages first: with stride-1 inputs a small first radix writes bank-conflicted
         const int rem = log2n % 4;
-        if (rem) radix[ns++] = 1 << rem;
         for (int i = 0; i < log2n / 4; ++i) radix[ns++] = 16;
+        if (rem) radix[ns++] = 1 << rem;
     } else {
         int a8 = log2n / 3, rem = log2n % 3;
         if (rem == 2) radix[ns++] = 4;
@@ -275,7 +326,7 @@ __device__ void lds_fft1(cx<T> *d, int log2n, const cx<T> *__restrict__ stw, int
         else if (R == 4) stockham1_stage<T, INV, 4, EPT>(d, log2n, lns, stw + off, tid, nthr);
         else if (R == 8) stockham1_stage<T, INV, 8, EPT>(d, log2n, lns, stw + off, tid, nthr);
         else if (EPT >= 16) stockham1_stage<T, INV, (EPT >= 16 ? 16 : 8), EPT>(d, log2n, lns, stw + off, tid, nthr);
-        off += (size_t)(1 << lns) * (R - 1);
+        off += (size_t)(1 << lns) * (R == 16 ? 6 : R == 8 ? 4 : 1);
         lns += (R == 2) ? 1 : (R == 4) ? 2 : (R == 8) ? 3 : 4;
     }
 }
@@ -290,7 +341,7 @@ constexpr int fft1_nstages_ct(int log2n, int ept) {
 constexpr int fft1_radix_ct(int log2n, int ept, int st) {
     if (ept >= 16) {
         const int rem = log2n % 4;
-        return (rem && st == 0) ? (1 << rem) : 16;
+        return (rem && st == log2n / 4) ? (1 << rem) : 16;
     }
     const int rem = log2n % 3;
     if (rem == 2) return st == 0 ? 4 : 8;
@@ -307,12 +358,34 @@ constexpr int fft1_log2ns_ct(int log2n, int ept, int st) {
 }
 constexpr int fft1_off_ct(int log2n, int ept, int st) {
     int off = 0;
-    for (int i = 0; i < st; ++i) off += (1 << fft1_log2ns_ct(log2n, ept, i)) * (fft1_radix_ct(log2n, ept, i) - 1);
+    for (int i = 0; i < st; ++i) off += (1 << fft1_log2ns_ct(log2n, ept, i)) * tw_per_k(fft1_radix_ct(log2n, ept, i));
     return off;
 }
 
+// number of table entries a thread loads for stage ST (NB butterflies)
+constexpr int fft1_twl_ct(int log2n, int ept, int st) {
+    return (st < fft1_nstages_ct(log2n, ept) && fft1_log2ns_ct(log2n, ept, st) > 0)
+               ? (ept / fft1_radix_ct(log2n, ept, st)) * tw_per_k(fft1_radix_ct(log2n, ept, st))
+               : 0;
+}
+
+template <typename T, int EPT, int LOG2N, int ST>
+__device__ __forceinline__ void fft1_tw_load_ct(const cx<T> *__restrict__ stw, int tid, cx<T> *wl) {
+    if constexpr (fft1_twl_ct(LOG2N, EPT, ST) > 0) {
+        constexpr int R = fft1_radix_ct(LOG2N, EPT, ST), NB = EPT / R, TWN = tw_per_k(R);
+        constexpr int NS = 1 << fft1_log2ns_ct(LOG2N, EPT, ST), NTHR = (1 << LOG2N) / EPT;
+        const cx<T> *t = stw + fft1_off_ct(LOG2N, EPT, ST);
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            const int k = (tid + i * NTHR) & (NS - 1);
+#pragma unroll
+            for (int q = 0; q < TWN; ++q) wl[i * TWN + q] = t[k * TWN + q];
+        }
+    }
+}
+
 template <typename T, bool INV, int R, int EPT, int LOG2N, int LOG2NS>
-__device__ __forceinline__ void stockham1_stage_ct(cx<T> *d, const cx<T> *__restrict__ stw, int tid) {
+__device__ __forceinline__ void stockham1_stage_ct(cx<T> *d, const cx<T> *wl, int tid) {
     constexpr int NB = EPT / R;
     constexpr int LR = (R == 2) ? 1 : (R == 4) ? 2 : (R == 8) ? 3 : 4;
     constexpr int NBF = 1 << (LOG2N - LR);
@@ -324,16 +397,14 @@ __device__ __forceinline__ void stockham1_stage_ct(cx<T> *d, const cx<T> *__rest
     for (int i = 0; i < NB; ++i) {
         const int j = tid + i * NTHR;
         const int k = j & (NS - 1);
-        const int jp = fpad(j);
+        const int jp = fsw(j);
 #pragma unroll
-        for (int r = 0; r < R; ++r) v[i * R + r] = d[(NBF % 16 == 0) ? jp + r * (NBF + NBF / 16) : fpad(j + r * NBF)];
-        if (LOG2NS > 0) {
+        for (int r = 0; r < R; ++r) v[i * R + r] = d[(NBF % 256 == 0) ? jp + r * NBF : fsw(j + r * NBF)];
+        if constexpr (LOG2NS > 0) {
+            cx<T> w[R];
+            tw_expand<T, INV, R>(wl + i * tw_per_k(R), w);
 #pragma unroll
-            for (int r = 1; r < R; ++r) {
-                cx<T> w = stw[k * (R - 1) + r - 1];
-                if (INV) w.y = -w.y;
-                v[i * R + r] = cmul(v[i * R + r], w);
-            }
+            for (int r = 1; r < R; ++r) v[i * R + r] = cmul(v[i * R + r], w[r]);
         }
         dftR<T, INV, R>(&v[i * R]);
         base_out[i] = ((j - k) << LR) + k;
@@ -341,27 +412,33 @@ __device__ __forceinline__ void stockham1_stage_ct(cx<T> *d, const cx<T> *__rest
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-        const int bp = fpad(base_out[i]);
+        const int bp = fsw(base_out[i]);
 #pragma unroll
-        for (int r = 0; r < R; ++r)
-            d[(NS % 16 == 0) ? bp + r * (NS + NS / 16) : fpad(base_out[i] + r * NS)] = v[i * R + r];
+        for (int r = 0; r < R; ++r) d[(NS % 256 == 0) ? bp + r * NS : fsw(base_out[i] + r * NS)] = v[i * R + r];
     }
     __syncthreads();
 }
 
+// Stage ST runs with its table entries already in registers (wl) while the
+// next stage's entries are in flight.
 template <typename T, bool INV, int EPT, int LOG2N, int ST>
-__device__ __forceinline__ void lds_fft1_ct_from(cx<T> *d, const cx<T> *__restrict__ stw, int tid) {
+__device__ __forceinline__ void lds_fft1_ct_from(cx<T> *d, const cx<T> *__restrict__ stw, int tid, const cx<T> *wl) {
     if constexpr (ST < fft1_nstages_ct(LOG2N, EPT)) {
         constexpr int R = fft1_radix_ct(LOG2N, EPT, ST);
-        stockham1_stage_ct<T, INV, R, EPT, LOG2N, fft1_log2ns_ct(LOG2N, EPT, ST)>(
-            d, stw + fft1_off_ct(LOG2N, EPT, ST), tid);
-        lds_fft1_ct_from<T, INV, EPT, LOG2N, ST + 1>(d, stw, tid);
+        constexpr int NXT = fft1_twl_ct(LOG2N, EPT, ST + 1);
+        cx<T> wn[NXT > 0 ? NXT : 1];
+        fft1_tw_load_ct<T, EPT, LOG2N, ST + 1>(stw, tid, wn);
+        stockham1_stage_ct<T, INV, R, EPT, LOG2N, fft1_log2ns_ct(LOG2N, EPT, ST)>(d, wl, tid);
+        lds_fft1_ct_from<T, INV, EPT, LOG2N, ST + 1>(d, stw, tid, wn);
     }
 }
 
 template <typename T, bool INV, int EPT, int LOG2N>
 __device__ __forceinline__ void lds_fft1_ct(cx<T> *d, const cx<T> *__restrict__ stw, int tid) {
-    lds_fft1_ct_from<T, INV, EPT, LOG2N, 0>(d, stw, tid);
+    constexpr int N0 = fft1_twl_ct(LOG2N, EPT, 0);
+    cx<T> w0[N0 > 0 ? N0 : 1];
+    fft1_tw_load_ct<T, EPT, LOG2N, 0>(stw, tid, w0);
+    lds_fft1_ct_from<T, INV, EPT, LOG2N, 0>(d, stw, tid, w0);
 }
 
 }  // namespace sg
