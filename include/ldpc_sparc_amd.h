@@ -168,6 +168,36 @@ int sg_ldpc_count_errors_device(sg_graph *g, int precision, const void *d_app, c
                                 const int32_t *d_it, int B, int k, int64_t *d_counts,
                                 void *stream);
 
+/* ------------------------------------------------- integrated AMP <-> BP */
+/* The integrated decoders of sparc_sophie/sparc_new.py on a dense design
+ * plan and an LDPC graph; every L log2 M bits of a codeword are LDPC
+ * protected (ldpc_bp asserts it, sparc_new.py:1171).  mode:
+ *   SG_INT_NAIVE       naively_integrated_decoder :257-282
+ *   SG_INT_NAIVE_POST  naively_integrated_decoder_posteriors :411-439
+ *   SG_INT_DIFF        integrated_decoder :472-502 (differentiated eta :824-841)
+ *   SG_INT_DIFF_POST   integrated_decoder_posteriors :675-705 (:843-869)
+ * y [B][n] -> bits [B][(L log2 M / N) K] (app[:K] < 0 of the final decode,
+ * bp_its_final iterations; bp_its per intermediate decode; the reference uses
+ * 6 and 200, sumprod2).  tau2 [B][t_max] (optional) receives tau^2 of every
+ * iteration. */
+enum sg_integrated_mode { SG_INT_NAIVE = 0, SG_INT_NAIVE_POST = 1, SG_INT_DIFF = 2, SG_INT_DIFF_POST = 3 };
+int sg_integrated_decode(sg_dense_plan *p, sg_graph *g, int mode, int K, const double *y, int B, int t_max,
+                         int bp_its, int bp_its_final, uint8_t *bits, double *tau2);
+int sg_integrated_decode_device(sg_dense_plan *p, sg_graph *g, int mode, int K, const void *d_y, int B,
+                                int t_max, int bp_its, int bp_its_final, uint8_t *d_bits, double *d_tau2,
+                                void *stream);
+/* The soft-glue functions on host arrays, batched over B codewords:
+ * bp_output_to_beta_estimate :1260-1279 (probs [B][L log2 M] -> beta [B][L M]),
+ * update_using_bp_probs :1030-1038, differentiated_eta_calc(_posteriors)
+ * :824-869 (tau2 [B]; gamma ignored unless posteriors). */
+int sg_bp_output_to_beta(int precision, const double *probs, int B, int L, int M, double sqrt_nPl,
+                         double *beta);
+int sg_update_using_bp_probs(int precision, const double *gamma, const double *alpha, int B, int L, int M,
+                             double sqrt_nPl, double *beta);
+int sg_differentiated_eta(int precision, int posteriors, const double *beta, const double *gamma,
+                          const double *alpha, const double *vk, const double *vk0, const double *tau2, int B,
+                          int L, int M, double sqrt_nPl, double *out);
+
 /* Reference-compatible scalar entry points: exact signatures of the ctypes
  * targets in ldpc.py:481-503 (c_ldpc.c:32,138,234,294,339) with Linux LP64
  * `long`.  Each call decodes one codeword on the GPU in double precision. */

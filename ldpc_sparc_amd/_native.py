@@ -100,7 +100,20 @@ SIGNATURES = [
                                                  ct.c_int, ct.c_int, ct.c_int, vp, vp]),
     ("sg_beta_to_llr_device", ct.c_int, [ct.c_int, vp, ct.c_int, ct.c_int, ct.c_int, ct.c_double, ct.c_int,
                                          ct.c_int, ct.c_int, ct.c_int, vp, vp]),
+    # integrated AMP <-> BP decoders
+    ("sg_integrated_decode", ct.c_int, [vp, vp, ct.c_int, ct.c_int, vp, ct.c_int, ct.c_int, ct.c_int, ct.c_int,
+                                        vp, vp]),
+    ("sg_integrated_decode_device", ct.c_int, [vp, vp, ct.c_int, ct.c_int, vp, ct.c_int, ct.c_int, ct.c_int,
+                                               ct.c_int, vp, vp, vp]),
+    ("sg_bp_output_to_beta", ct.c_int, [ct.c_int, vp, ct.c_int, ct.c_int, ct.c_int, ct.c_double, vp]),
+    ("sg_update_using_bp_probs", ct.c_int, [ct.c_int, vp, vp, ct.c_int, ct.c_int, ct.c_int, ct.c_double, vp]),
+    ("sg_differentiated_eta", ct.c_int, [ct.c_int, ct.c_int, vp, vp, vp, vp, vp, vp, ct.c_int, ct.c_int, ct.c_int,
+                                         ct.c_double, vp]),
 ]
+
+SG_INT_NAIVE, SG_INT_NAIVE_POST, SG_INT_DIFF, SG_INT_DIFF_POST = 0, 1, 2, 3
+INTEGRATED_MODES = {"naive": SG_INT_NAIVE, "naive_posteriors": SG_INT_NAIVE_POST, "integrated": SG_INT_DIFF,
+                    "integrated_posteriors": SG_INT_DIFF_POST}
 
 SG_PH_COUNT = 8
 

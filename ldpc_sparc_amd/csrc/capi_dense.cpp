@@ -2,6 +2,8 @@
 // of the AMP -> BP glue (sparc_new.py:1118-1193).
 #include <algorithm>
 #include <cmath>
+#include <initializer_list>
+#include <utility>
 #include <vector>
 
 #include "dense.hpp"
@@ -18,6 +20,14 @@ struct sg_dense_plan {
     int32_t *ws_idx = nullptr;
     void *ws_io = nullptr;
     size_t ws_io_bytes = 0;
+    // integrated decoders (integrated.hip): weighted alpha, gamma [B][LM];
+    // bit probabilities vk0, vk, LLRs and app [B][L log M]; BP iteration counts;
+    // per-section / per-codeword sums of the differentiated eta
+    int cap_Bi = 0;
+    void *wi_alpha = nullptr, *wi_gamma = nullptr, *wi_vk0 = nullptr, *wi_vk = nullptr, *wi_llr = nullptr,
+         *wi_app = nullptr;
+    int32_t *wi_it = nullptr;
+    double *wi_part = nullptr, *wi_ons = nullptr;
 };
 
 namespace sg {
@@ -52,6 +62,34 @@ static int dense_ensure_ws(sg_dense_plan *p, int B) {
     return SG_OK;
 }
 
+static void integ_free_ws(sg_dense_plan *p) {
+    void *bufs[] = {p->wi_alpha, p->wi_gamma, p->wi_vk0, p->wi_vk, p->wi_llr, p->wi_app, p->wi_it, p->wi_part,
+                    p->wi_ons};
+    for (void *b : bufs)
+        if (b) hipFree(b);
+    p->wi_alpha = p->wi_gamma = p->wi_vk0 = p->wi_vk = p->wi_llr = p->wi_app = nullptr;
+    p->wi_it = nullptr;
+    p->wi_part = p->wi_ons = nullptr;
+    p->cap_Bi = 0;
+}
+
+static int integ_ensure_ws(sg_dense_plan *p, int B, int nbits) {
+    if (B <= p->cap_Bi) return SG_OK;
+    integ_free_ws(p);
+    const size_t rs = rsize(p), Bz = (size_t)B;
+    SG_HIP(hipMalloc(&p->wi_alpha, Bz * p->LM * rs));
+    SG_HIP(hipMalloc(&p->wi_gamma, Bz * p->LM * rs));
+    SG_HIP(hipMalloc(&p->wi_vk0, Bz * nbits * rs));
+    SG_HIP(hipMalloc(&p->wi_vk, Bz * nbits * rs));
+    SG_HIP(hipMalloc(&p->wi_llr, Bz * nbits * rs));
+    SG_HIP(hipMalloc(&p->wi_app, Bz * nbits * rs));
+    SG_HIP(hipMalloc(&p->wi_it, Bz * nbits * sizeof(int32_t)));
+    SG_HIP(hipMalloc(&p->wi_part, Bz * p->L * sizeof(double)));
+    SG_HIP(hipMalloc(&p->wi_ons, Bz * sizeof(double)));
+    p->cap_Bi = B;
+    return SG_OK;
+}
+
 static int dense_ensure_io(sg_dense_plan *p, size_t bytes) {
     if (bytes <= p->ws_io_bytes) return SG_OK;
     if (p->ws_io) hipFree(p->ws_io);
@@ -69,6 +107,8 @@ static DenseBufs<T> dbufs(const sg_dense_plan *p, int B, const void *y) {
     d.y = (const T *)(y ? y : p->ws_y); d.z = (T *)p->ws_z; d.beta = (T *)p->ws_beta; d.s = (T *)p->ws_s;
     d.part = (T *)p->ws_part; d.nsplit = p->nsplit; d.tau2 = p->ws_tau2; d.bsq = nullptr;
     d.sec_bsq = p->ws_sec_bsq;
+    d.ons_mode = 0;
+    d.ons = nullptr;
     return d;
 }
 
@@ -178,6 +218,132 @@ static int iteration_impl(sg_dense_plan *p, const double *y, const double *beta,
     return SG_OK;
 }
 
+
+// The AMP <-> BP integrated decoders (sparc_new.py:257-282 naive, :411-439
+// naive posteriors, :472-502 integrated, :675-705 integrated posteriors) for a
+// batch sharing the design: every LDPC block of every codeword goes through
+// one batched BP launch per iteration.  bits [B][nblk K] = app[:K] < 0 of the
+// final 200-iteration (bp_its_final) decode; tau_hist [B][t_max] optional.
+template <typename T>
+static int integ_impl(sg_dense_plan *p, sg_graph *g, int mode, int N, int K, const void *d_y, int B, int t_max,
+                      int its, int its_final, uint8_t *d_bits, double *d_tau_hist, hipStream_t s) {
+    const int logM = [&] { int k = 0; while ((1 << k) < p->M) ++k; return k; }();
+    const int nbits = p->L * logM, nblk = nbits / N;
+    SG_TRY(dense_ensure_ws(p, B));
+    SG_TRY(integ_ensure_ws(p, B, nbits));
+    DenseBufs<T> d = dbufs<T>(p, B, d_y);
+    const double snp = std::sqrt((double)p->n * (p->P / p->L));
+    const bool naive = mode == SG_INT_NAIVE || mode == SG_INT_NAIVE_POST;
+    const bool post = mode == SG_INT_NAIVE_POST || mode == SG_INT_DIFF_POST;
+    T *alpha_w = (T *)p->wi_alpha, *gamma = (T *)p->wi_gamma, *vk0 = (T *)p->wi_vk0, *vk = (T *)p->wi_vk;
+    T *llr = (T *)p->wi_llr, *app = (T *)p->wi_app;
+    const size_t nb = (size_t)B * nbits;
+    const int prec = sizeof(T) == 8 ? SG_F64 : SG_F32;
+    SG_HIP(hipMemsetAsync(p->ws_beta, 0, (size_t)B * p->LM * sizeof(T), s));
+    SG_HIP(hipMemsetAsync(p->ws_sec_bsq, 0, (size_t)B * p->L * sizeof(double), s));
+    DenseBufs<T> da = d;  // eta writes the weighted alpha (the MMSE estimate) here
+    da.beta = alpha_w;
+    if (!naive) {
+        d.ons_mode = mode == SG_INT_DIFF ? 1 : 2;
+        d.ons = p->wi_ons;
+    }
+    for (int t = 0; t < t_max; ++t) {
+        if (!naive && t > 0)  // sum of the differentiated eta with the previous tau^2
+            SG_TRY(integ_launch_deta<T>(post ? 1 : 0, d.beta, gamma, alpha_w, snp, vk, vk0, p->ws_tau2, B, p->L, p->M,
+                                        snp, p->wi_part, p->wi_ons, (T *)nullptr, s));
+        if (t > 0) SG_TRY(dense_launch_ab<T>(d, s));
+        SG_TRY(dense_launch_residual<T>(d, t, s));  // z; tau^2 = ||z||^2 / n
+        SG_TRY(dense_launch_az<T>(d, s));            // s = beta + A^T z
+        if (d_tau_hist)
+            SG_HIP(hipMemcpy2DAsync(d_tau_hist + t, (size_t)t_max * 8, p->ws_tau2, 8, 8, B, hipMemcpyDeviceToDevice, s));
+        SG_TRY(dense_launch_eta<T>(da, s));
+        SG_TRY(glue_launch_llr<T>(alpha_w, B, p->L, p->M, 0, p->L, 1.0 / snp, nbits, vk0, 1, s));  // P(bit = 0)
+        SG_TRY(integ_launch_llr<T>(vk0, nb, llr, s));
+        if (t == t_max - 1) {
+            SG_TRY(sg_ldpc_decode_device(g, SG_SUMPROD2, prec, llr, B * nblk, its_final, 0.7, app, p->wi_it, s));
+            SG_TRY(integ_launch_hard_bits<T>(app, B * nblk, N, K, d_bits, s));
+            break;
+        }
+        SG_TRY(sg_ldpc_decode_device(g, SG_SUMPROD2, prec, llr, B * nblk, its, 0.7, app, p->wi_it, s));
+        SG_TRY(integ_launch_probs<T>(app, nb, vk, s));
+        if (!post) {
+            SG_TRY(integ_launch_bp_to_beta<T>(vk, B, p->L, p->M, snp, 0, d.beta, s));
+        } else {
+            SG_TRY(integ_launch_bp_to_beta<T>(vk, B, p->L, p->M, snp, 1, gamma, s));
+            SG_TRY(integ_launch_update<T>(gamma, alpha_w, snp, B, p->L, p->M, snp, d.beta, s));
+        }
+        if (naive) SG_TRY(dense_launch_bsq<T>(d, s));  // ||beta||^2 of the BP-derived beta for the Onsager term
+    }
+    return SG_OK;
+}
+
+// The soft-glue pieces on host arrays (the reference's functions, batched over B).
+template <typename F>
+static int integ_host_call(int precision, std::initializer_list<std::pair<const double *, size_t>> ins,
+                           std::initializer_list<std::pair<double *, size_t>> outs, F &&launch) {
+    SG_CHECK_ARG(precision == SG_F32 || precision == SG_F64, "bad precision");
+    SG_TRY(ensure_device());
+    hipStream_t s = lib_stream();
+    const size_t rs = precision == SG_F64 ? 8 : 4;
+    std::vector<void *> dev;
+    auto cleanup = [&] {
+        for (void *v : dev) hipFree(v);
+    };
+    int rc = SG_OK;
+    std::vector<void *> din, dout;
+    for (auto &in : ins) {
+        void *a = nullptr, *st = nullptr;
+        if (hipMalloc(&a, std::max<size_t>(1, in.second * rs)) != hipSuccess ||
+            hipMalloc(&st, std::max<size_t>(1, in.second * 8)) != hipSuccess) {
+            if (a) hipFree(a);
+            if (st) hipFree(st);
+            cleanup();
+            return fail(SG_ERR_NOMEM, "device buffers");
+        }
+        dev.push_back(a);
+        dev.push_back(st);
+        if (in.first) {
+            if (hipMemcpyAsync(st, in.first, in.second * 8, hipMemcpyHostToDevice, s) != hipSuccess) rc = SG_ERR_HIP;
+            if (precision == SG_F64)
+                hipMemcpyAsync(a, st, in.second * 8, hipMemcpyDeviceToDevice, s);
+            else
+                hipLaunchKernelGGL(cast_to<float>, dim3(grid_for(in.second)), dim3(256), 0, s, (const double *)st,
+                                   (float *)a, in.second);
+        }
+        din.push_back(in.first ? a : nullptr);
+    }
+    for (auto &o : outs) {
+        void *a = nullptr, *st = nullptr;
+        if (hipMalloc(&a, std::max<size_t>(1, o.second * rs)) != hipSuccess ||
+            hipMalloc(&st, std::max<size_t>(1, o.second * 8)) != hipSuccess) {
+            if (a) hipFree(a);
+            if (st) hipFree(st);
+            cleanup();
+            return fail(SG_ERR_NOMEM, "device buffers");
+        }
+        dev.push_back(a);
+        dev.push_back(st);
+        dout.push_back(a);
+        dout.push_back(st);
+    }
+    if (rc == SG_OK) rc = launch(din, dout, s);
+    size_t k = 0;
+    for (auto &o : outs) {
+        void *a = dout[2 * k], *st = dout[2 * k + 1];
+        ++k;
+        if (rc != SG_OK) break;
+        if (precision == SG_F64)
+            hipMemcpyAsync(st, a, o.second * 8, hipMemcpyDeviceToDevice, s);
+        else
+            hipLaunchKernelGGL(cast_from<float>, dim3(grid_for(o.second)), dim3(256), 0, s, (const float *)a,
+                               (double *)st, o.second);
+        if (hipMemcpyAsync(o.first, st, o.second * 8, hipMemcpyDeviceToHost, s) != hipSuccess) rc = SG_ERR_HIP;
+    }
+    if (hipStreamSynchronize(s) != hipSuccess && rc == SG_OK) rc = SG_ERR_HIP;
+    cleanup();
+    return rc == SG_OK ? SG_OK : fail(rc, "integrated glue call failed");
+}
+
 }  // namespace sg
 
 using namespace sg;
@@ -232,6 +398,7 @@ int sg_dense_plan_create_random(int n, int L, int M, double P, uint64_t seed, in
 int sg_dense_plan_destroy(sg_dense_plan *p) {
     if (!p) return SG_OK;
     dense_free_ws(p);
+    integ_free_ws(p);
     if (p->A) hipFree(p->A);
     delete p;
     return SG_OK;
@@ -380,6 +547,116 @@ int sg_concat_count_errors_device(int precision, const int32_t *d_map_idx, const
                                              d_info, mults, N, K, d_counts, s)
                : concat_launch_count<float>(d_map_idx, d_true_idx, B, L, L_unprotected, logM, (const float *)d_app,
                                             d_info, mults, N, K, d_counts, s);
+}
+
+int sg_integrated_decode_device(sg_dense_plan *p, sg_graph *g, int mode, int K, const void *d_y, int B, int t_max,
+                                int bp_its, int bp_its_final, uint8_t *d_bits, double *d_tau2, void *stream) {
+    SG_CHECK_ARG(p && g && d_y && d_bits, "null argument");
+    SG_CHECK_ARG(mode >= SG_INT_NAIVE && mode <= SG_INT_DIFF_POST, "unknown integrated decoder %d", mode);
+    SG_CHECK_ARG(t_max >= 1 && bp_its >= 0 && bp_its_final >= 0, "bad iteration counts");
+    int N = 0, nc = 0;
+    SG_TRY(sg_ldpc_graph_info(g, &N, &nc, nullptr, nullptr, nullptr));
+    int logM = 0;
+    while ((1 << logM) < p->M) ++logM;
+    SG_CHECK_ARG(N > 0 && (p->L * logM) % N == 0, "L log2 M = %d bits must be a multiple of the block length %d",
+                 p->L * logM, N);  // ldpc_bp's assert (sparc_new.py:1171)
+    SG_CHECK_ARG(K > 0 && K <= N, "bad information length %d", K);
+    if (B <= 0) return SG_OK;
+    SG_TRY(ensure_device());
+    SG_HIP(hipSetDevice(p->device));
+    hipStream_t s = pick_stream(stream);
+    return p->precision == SG_F64
+               ? integ_impl<double>(p, g, mode, N, K, d_y, B, t_max, bp_its, bp_its_final, d_bits, d_tau2, s)
+               : integ_impl<float>(p, g, mode, N, K, d_y, B, t_max, bp_its, bp_its_final, d_bits, d_tau2, s);
+}
+
+int sg_integrated_decode(sg_dense_plan *p, sg_graph *g, int mode, int K, const double *y, int B, int t_max,
+                         int bp_its, int bp_its_final, uint8_t *bits, double *tau2) {
+    SG_CHECK_ARG(p && g && y && bits, "null argument");
+    if (B <= 0) return SG_OK;
+    SG_TRY(ensure_device());
+    SG_HIP(hipSetDevice(p->device));
+    int N = 0;
+    SG_TRY(sg_ldpc_graph_info(g, &N, nullptr, nullptr, nullptr, nullptr));
+    int logM = 0;
+    while ((1 << logM) < p->M) ++logM;
+    SG_CHECK_ARG(N > 0 && (p->L * logM) % N == 0, "L log2 M must be a multiple of the block length");
+    const size_t nbits = (size_t)B * (p->L * logM / N) * K;
+    hipStream_t s = lib_stream();
+    SG_TRY(dense_ensure_ws(p, B));
+    const size_t rs = rsize(p), ny = (size_t)B * p->n;
+    SG_TRY(dense_ensure_io(p, ny * 8 + nbits + (size_t)B * t_max * 8 + 64));
+    double *io = (double *)p->ws_io;
+    uint8_t *dbits = (uint8_t *)(io + ny);
+    double *dtau = (double *)((char *)p->ws_io + ((ny * 8 + nbits + 63) / 64) * 64);
+    SG_HIP(hipMemcpyAsync(io, y, ny * 8, hipMemcpyHostToDevice, s));
+    if (p->precision == SG_F32)  // cast into the plan's own y buffer
+        hipLaunchKernelGGL(cast_to<float>, dim3(grid_for(ny)), dim3(256), 0, s, (const double *)io, (float *)p->ws_y,
+                           ny);
+    const void *dy = p->precision == SG_F32 ? p->ws_y : (const void *)io;
+    (void)rs;
+    SG_TRY(sg_integrated_decode_device(p, g, mode, K, dy, B, t_max, bp_its, bp_its_final, dbits,
+                                       tau2 ? dtau : nullptr, s));
+    SG_HIP(hipMemcpyAsync(bits, dbits, nbits, hipMemcpyDeviceToHost, s));
+    if (tau2) SG_HIP(hipMemcpyAsync(tau2, dtau, (size_t)B * t_max * 8, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    return SG_OK;
+}
+
+int sg_bp_output_to_beta(int precision, const double *probs, int B, int L, int M, double sqrt_nPl, double *beta) {
+    SG_CHECK_ARG(probs && beta && B >= 0 && L > 0 && M > 1 && (M & (M - 1)) == 0, "bad argument");
+    int logM = 0;
+    while ((1 << logM) < M) ++logM;
+    const size_t np = (size_t)B * L * logM, nbeta = (size_t)B * L * M;
+    return integ_host_call(precision, {{probs, np}}, {{beta, nbeta}}, [&](auto &in, auto &out, hipStream_t s) {
+        return precision == SG_F64
+                   ? integ_launch_bp_to_beta<double>((const double *)in[0], B, L, M, sqrt_nPl, 0, (double *)out[0], s)
+                   : integ_launch_bp_to_beta<float>((const float *)in[0], B, L, M, sqrt_nPl, 0, (float *)out[0], s);
+    });
+}
+
+int sg_update_using_bp_probs(int precision, const double *gamma, const double *alpha, int B, int L, int M,
+                             double sqrt_nPl, double *beta) {
+    SG_CHECK_ARG(gamma && alpha && beta && B >= 0 && L > 0 && M > 0, "bad argument");
+    const size_t nn = (size_t)B * L * M;
+    return integ_host_call(precision, {{gamma, nn}, {alpha, nn}}, {{beta, nn}}, [&](auto &in, auto &out, hipStream_t s) {
+        return precision == SG_F64
+                   ? integ_launch_update<double>((const double *)in[0], (const double *)in[1], 1.0, B, L, M, sqrt_nPl,
+                                                 (double *)out[0], s)
+                   : integ_launch_update<float>((const float *)in[0], (const float *)in[1], 1.0, B, L, M, sqrt_nPl,
+                                                (float *)out[0], s);
+    });
+}
+
+int sg_differentiated_eta(int precision, int posteriors, const double *beta, const double *gamma,
+                          const double *alpha, const double *vk, const double *vk0, const double *tau2, int B, int L,
+                          int M, double sqrt_nPl, double *out) {
+    SG_CHECK_ARG(beta && alpha && vk && vk0 && tau2 && out && (!posteriors || gamma), "null argument");
+    SG_CHECK_ARG(B >= 0 && L > 0 && M > 1 && (M & (M - 1)) == 0, "bad shape");
+    int logM = 0;
+    while ((1 << logM) < M) ++logM;
+    const size_t nn = (size_t)B * L * M, nv = (size_t)B * L * logM;
+    SG_TRY(ensure_device());
+    double *dtau = nullptr, *dpart = nullptr;
+    SG_HIP(hipMalloc(&dtau, std::max<size_t>(1, B) * 8));
+    SG_HIP(hipMalloc(&dpart, std::max<size_t>(1, (size_t)B * L) * 8));
+    hipMemcpy(dtau, tau2, (size_t)B * 8, hipMemcpyHostToDevice);
+    const int rc = integ_host_call(
+        precision, {{beta, nn}, {gamma, gamma ? nn : 0}, {alpha, nn}, {vk, nv}, {vk0, nv}}, {{out, nn}},
+        [&](auto &in, auto &o, hipStream_t s) {
+            return precision == SG_F64
+                       ? integ_launch_deta<double>(posteriors ? 1 : 0, (const double *)in[0], (const double *)in[1],
+                                                   (const double *)in[2], 1.0, (const double *)in[3],
+                                                   (const double *)in[4], dtau, B, L, M, sqrt_nPl, dpart, nullptr,
+                                                   (double *)o[0], s)
+                       : integ_launch_deta<float>(posteriors ? 1 : 0, (const float *)in[0], (const float *)in[1],
+                                                  (const float *)in[2], 1.0, (const float *)in[3],
+                                                  (const float *)in[4], dtau, B, L, M, sqrt_nPl, dpart, nullptr,
+                                                  (float *)o[0], s);
+        });
+    hipFree(dtau);
+    hipFree(dpart);
+    return rc;
 }
 
 }  // extern "C"

@@ -172,7 +172,7 @@ __global__ __launch_bounds__(256) void residual_kernel(DenseBufs<T> d, int t, do
     __shared__ double sh_bsq;
     const int b = blockIdx.y, tid = threadIdx.x;
     const int i = blockIdx.x * 256 + tid;
-    if (t > 0 && tid < 64) {  // ||beta||^2 of the codeword, fixed order
+    if (t > 0 && d.ons_mode == 0 && tid < 64) {  // ||beta||^2 of the codeword, fixed order
         double v = 0.0;
         for (int l = tid; l < d.L; l += 64) v += d.sec_bsq[(long)b * d.L + l];
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -188,7 +188,10 @@ __global__ __launch_bounds__(256) void residual_kernel(DenseBufs<T> d, int t, do
                 T r = T(0);
                 for (int sp = 0; sp < d.nsplit; ++sp) r += d.part[((long)sp * d.B + b) * d.n + i];
                 const T zo = d.z[(long)b * d.npad + i];
-                const T ons = (zo / (T)d.tau2[b]) * (T)(d.P - sh_bsq / d.n);
+                T ons;
+                if (d.ons_mode == 1) ons = (zo / (T)d.n) * (T)d.ons[b];
+                else if (d.ons_mode == 2) ons = zo * (T)(d.ons[b] / d.n);
+                else ons = (zo / (T)d.tau2[b]) * (T)(d.P - sh_bsq / d.n);
                 zn = (y - r) + ons;
             } else {
                 zn = y;

@@ -23,6 +23,11 @@ struct DenseBufs {
     double *tau2;      // [B]   ||z||^2 / n
     double *bsq;       // [B]   ||beta||^2
     double *sec_bsq;   // [B][L] per-section sum beta^2 (deterministic reduction)
+    // Onsager term of the residual: 0 = (z / tau^2)(P - ||beta||^2 / n)
+    // (sparc_new.py:903-905); 1 = (z / n) * ons[b] (integrated_decoder :490);
+    // 2 = z * (ons[b] / n) (integrated_decoder_posteriors :693)
+    int ons_mode;
+    const double *ons;  // [B] sum of the differentiated eta
 };
 
 template <typename T>
@@ -42,6 +47,23 @@ int dense_launch_map(const T *s, int B, int L, int M, int32_t *idx, hipStream_t 
 template <typename T>
 int glue_launch_llr(const T *beta, int B, int L, int M, int l0, int nl, double inv_sqrt_nPl, int llr_ld, T *llr,
                     int probs_only, hipStream_t s);
+
+// integrated decoders (integrated.hip)
+template <typename T>
+int integ_launch_llr(const T *p, size_t nn, T *llr, hipStream_t s);
+template <typename T>
+int integ_launch_probs(const T *app, size_t nn, T *p, hipStream_t s);
+template <typename T>
+int integ_launch_bp_to_beta(const T *probs, int B, int L, int M, double snp, int as_gamma, T *out, hipStream_t s);
+template <typename T>
+int integ_launch_update(const T *gamma, const T *alpha_w, double ascale, int B, int L, int M, double snp, T *beta,
+                        hipStream_t s);
+template <typename T>
+int integ_launch_deta(int post, const T *beta, const T *gamma, const T *alpha_w, double ascale, const T *vk,
+                      const T *vk0, const double *tau2, int B, int L, int M, double snp, double *part, double *ons,
+                      T *out, hipStream_t s);
+template <typename T>
+int integ_launch_hard_bits(const T *app, int nblocks, int N, int K, uint8_t *bits, hipStream_t s);
 
 template <typename T>
 int concat_launch_count(const int32_t *map_idx, const int32_t *true_idx, int B, int L, int L_unp, int logM,

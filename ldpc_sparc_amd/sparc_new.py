@@ -9,9 +9,16 @@ libldpc_sparc_amd; the design matrix and the message bits are drawn on the
 host with the reference's numpy generators so that results are reproducible
 seed for seed (parity mode).
 
-Not provided (the fork's experimental decoder variants, SURVEY.md 2 "OUT OF
-SCOPE"): *_decode_loop/_test*, naively_integrated_*, integrated_*, eta*,
-differentiated_eta_calc*, sparc_amp_loop/_termination.
+The AMP <-> BP integrated decoders (naively_integrated_decoder :257-282,
+naively_integrated_decoder_posteriors :411-439, integrated_decoder :472-502,
+integrated_decoder_posteriors :675-705) run as one batched device loop
+(sg_integrated_decode); their pieces (eta :709-735, eta_posteriors :793-822,
+differentiated_eta_calc(_posteriors) :824-869, update_using_bp_probs
+:1030-1038, bp_output_to_beta_estimate :1260-1279) are available on their
+own.  integrated_decode_batch decodes many received words sharing one design.
+
+Not provided (the fork's diagnostic variants): *_decode_loop,
+*_test*, sparc_amp_loop/_termination, no_onsager_decoder.
 
 Engine knobs (absent from the reference): decode_params may carry
 'precision' ('f64' default; 'f32' runs the products on the matrix cores).
@@ -333,3 +340,141 @@ def bit_err_rate(bits_in, bits_out):
     """Fraction of differing bits (sparc_new.py:1380-1388)."""
     assert len(bits_in == bits_out)
     return np.sum(bits_in != bits_out) / len(bits_in)
+
+
+# ------------------------------------------------------------------ integrated AMP <-> BP decoders
+
+
+def integrated_decode_batch(Y, design, c, mode, t_max, num_its=6, num_its_final=200, precision=_native.SG_F64):
+    """Batched integrated decoding of received words sharing one design.
+    mode: 'naive' | 'naive_posteriors' | 'integrated' | 'integrated_posteriors'.
+    Returns (information bits uint8 [B, blocks*K], tau^2 [B, t_max])."""
+    Y = np.ascontiguousarray(Y, dtype=np.float64)
+    if Y.ndim != 2 or Y.shape[1] != design.n:
+        raise ValueError(f"received words must have shape [B, {design.n}]")
+    logM = int(np.log2(design.M))
+    assert (design.L * logM) % c.N == 0  # ldpc_bp (sparc_new.py:1171)
+    B = Y.shape[0]
+    bits = np.zeros((B, design.L * logM // c.N * c.K), dtype=np.uint8)
+    tau2 = np.zeros((B, int(t_max)))
+    _native.check(_native.lib().sg_integrated_decode(
+        design.plan(precision), c._device_graph(), _native.INTEGRATED_MODES[mode], int(c.K), _native.ptr(Y), B,
+        int(t_max), int(num_its), int(num_its_final), _native.ptr(bits), _native.ptr(tau2)))
+    return bits, tau2
+
+
+def _integrated(mode, y, sparc_params, ldpc_params, decode_params, A):
+    P, L, M = sparc_params['P'], sparc_params['L'], sparc_params['M']
+    c = code(ldpc_params["standard"], ldpc_params["rate"], ldpc_params["z"])
+    design = _design_for(A, P, L, M)
+    bits, _ = integrated_decode_batch(np.asarray(y)[None, :], design, c, mode, decode_params['t_max'],
+                                      precision=_precision(decode_params))
+    return bits[0].astype(int)
+
+
+def naively_integrated_decoder(y, sparc_params, ldpc_params, decode_params, A):
+    """AMP iteration, then 6 BP iterations whose output replaces beta; final
+    200-iteration BP (sparc_new.py:257-282).  Returns the information bits."""
+    return _integrated("naive", y, sparc_params, ldpc_params, decode_params, A)
+
+
+def naively_integrated_decoder_posteriors(y, sparc_params, ldpc_params, decode_params, A):
+    """As naively_integrated_decoder with beta updated by the BP posteriors
+    (update_using_bp_probs) instead of replaced (sparc_new.py:411-439)."""
+    return _integrated("naive_posteriors", y, sparc_params, ldpc_params, decode_params, A)
+
+
+def integrated_decoder(y, sparc_params, ldpc_params, decode_params, A):
+    """AMP with BP inside the denoiser and the differentiated-eta Onsager term
+    (sparc_new.py:472-502)."""
+    return _integrated("integrated", y, sparc_params, ldpc_params, decode_params, A)
+
+
+def integrated_decoder_posteriors(y, sparc_params, ldpc_params, decode_params, A):
+    """integrated_decoder with the posterior update and its derivative
+    (sparc_new.py:675-705)."""
+    return _integrated("integrated_posteriors", y, sparc_params, ldpc_params, decode_params, A)
+
+
+def bp_output_to_beta_estimate(ldpc_probs, L, M, sqrt_nP_l):
+    """Section estimate from bit probabilities: prod of p (bit 0) or 1 - p
+    (bit 1) over the MSB-first bits, times sqrt(n P_l) (sparc_new.py:1260-1279)."""
+    _native.require_gpu()
+    p = np.ascontiguousarray(ldpc_probs, dtype=np.float64)
+    logM = int(np.log2(M))
+    assert p.size == L * logM
+    out = np.empty(L * M)
+    _native.check(_native.lib().sg_bp_output_to_beta(_native.SG_F64, _native.ptr(p), 1, int(L), int(M),
+                                                     float(sqrt_nP_l), _native.ptr(out)))
+    return out
+
+
+def update_using_bp_probs(gamma, alpha, sqrt_nP_l, M):
+    """sqrt(n P_l) (alpha gamma) normalised per section (sparc_new.py:1030-1038)."""
+    _native.require_gpu()
+    g = np.ascontiguousarray(gamma, dtype=np.float64)
+    a = np.ascontiguousarray(alpha, dtype=np.float64)
+    out = np.empty_like(a)
+    _native.check(_native.lib().sg_update_using_bp_probs(_native.SG_F64, _native.ptr(g), _native.ptr(a), 1,
+                                                         a.size // M, int(M), float(sqrt_nP_l), _native.ptr(out)))
+    return out
+
+
+def _deta(post, gamma, beta, vk, vk_0, alpha, tau_sqr, L, M, S_k, n, P_l):
+    _native.require_gpu()
+    if S_k is not None and [list(x) for x in S_k] != S_k_mapping(M):
+        raise ValueError("S_k must be S_k_mapping(M)")
+    arrs = [np.ascontiguousarray(v, dtype=np.float64) for v in (beta, alpha, vk, vk_0)]
+    g = np.ascontiguousarray(gamma, dtype=np.float64) if post else None
+    out = np.empty(L * M)
+    t = np.array([float(tau_sqr)])
+    _native.check(_native.lib().sg_differentiated_eta(
+        _native.SG_F64, int(post), _native.ptr(arrs[0]), _native.ptr(g) if post else None, _native.ptr(arrs[1]),
+        _native.ptr(arrs[2]), _native.ptr(arrs[3]), _native.ptr(t), 1, int(L), int(M), float(np.sqrt(n * P_l)),
+        _native.ptr(out)))
+    return out
+
+
+def differentiated_eta_calc(beta, vk, vk_0, alpha, tau_sqr, L, M, S_k, n, P_l):
+    """beta * d eta / d s of the BP-aided denoiser (sparc_new.py:824-841, sub_term
+    :871-883), in closed form on the GPU."""
+    return _deta(False, None, beta, vk, vk_0, alpha, tau_sqr, L, M, S_k, n, P_l)
+
+
+def differentiated_eta_calc_posteriors(gamma, beta, vk, vk_0, alpha, tau_sqr, L, M, S_k, n, P_l):
+    """Derivative of the posterior-updated denoiser (sparc_new.py:843-869)."""
+    return _deta(True, gamma, beta, vk, vk_0, alpha, tau_sqr, L, M, S_k, n, P_l)
+
+
+def eta(s, tau_sqr, n, P_l, M, L, c, num_its, num_its_final, hard_decision_bool):
+    """BP-aided denoiser (sparc_new.py:709-735): returns
+    (alpha, vk_0, vk, beta, hard_decision_bits)."""
+    sqrt_nP_l = np.sqrt(n * P_l)
+    weighted_alpha = msg_vector_mmse_estimator(s, tau_sqr, n, P_l, M)
+    alpha = weighted_alpha / sqrt_nP_l
+    vk_0 = beta_estimate_to_bp_probs(weighted_alpha, L, M, sqrt_nP_l)
+    if hard_decision_bool:
+        vk, hard_decision_bits = ldpc_bp(vk_0, c, num_its_final, True)
+        beta = np.zeros(L * M)
+    else:
+        vk, hard_decision_bits = ldpc_bp(vk_0, c, num_its, False)
+        beta = bp_output_to_beta_estimate(vk, L, M, sqrt_nP_l)
+    return alpha, vk_0, vk, beta, hard_decision_bits
+
+
+def eta_posteriors(s, tau_sqr, n, P_l, M, L, c, num_its, num_its_final, hard_decision_bool):
+    """Posterior-updating denoiser (sparc_new.py:793-822): returns
+    (alpha, vk_0, vk, beta, gamma, hard_decision_bits)."""
+    sqrt_nP_l = np.sqrt(n * P_l)
+    weighted_alpha = msg_vector_mmse_estimator(s, tau_sqr, n, P_l, M)
+    alpha = weighted_alpha / sqrt_nP_l
+    vk_0 = beta_estimate_to_bp_probs(weighted_alpha, L, M, sqrt_nP_l)
+    if hard_decision_bool:
+        vk, hard_decision_bits = ldpc_bp(vk_0, c, num_its_final, True)
+        beta = np.zeros(L * M)
+        gamma = np.zeros(L * M)
+    else:
+        vk, hard_decision_bits = ldpc_bp(vk_0, c, num_its, False)
+        gamma = bp_output_to_beta_estimate(vk, L, M, sqrt_nP_l) / sqrt_nP_l
+        beta = update_using_bp_probs(gamma, alpha, sqrt_nP_l, M)
+    return alpha, vk_0, vk, beta, gamma, hard_decision_bits

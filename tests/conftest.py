@@ -40,3 +40,9 @@ def sparc_golden():
 def sophie_golden():
     import numpy as np
     return np.load(os.path.join(REPO, "tests", "golden", "sophie_golden.npz"))
+
+
+@pytest.fixture(scope="session")
+def integrated_golden():
+    import numpy as np
+    return np.load(os.path.join(REPO, "tests", "golden", "integrated_golden.npz"))
