@@ -168,6 +168,29 @@ int sg_ldpc_count_errors_device(sg_graph *g, int precision, const void *d_app, c
                                 const int32_t *d_it, int B, int k, int64_t *d_counts,
                                 void *stream);
 
+/* ------------------------------------------- device encoder and channel */
+/* Throughput-mode generation, keyed by Philox4x32-10
+ * counters (seed, stream_id, codeword index, element): results depend only on
+ * the key, not on B, the grid or the rank.  Parity mode (the reference's
+ * numpy generators, seed for seed) stays on the host. */
+/* nbits random bits per row, d_bits [B][nbits] uint8 (ldpc_awgn.py:44 / sparc.py:174-180) */
+int sg_rng_bits_device(uint64_t seed, uint64_t stream_id, int B, int nbits, uint8_t *d_bits, void *stream);
+/* section indices from MSB-first bit groups (sparc.py:330-364): d_bits [B][L*logM] -> d_idx [B][L] */
+int sg_bits_to_sections_device(const uint8_t *d_bits, int B, int L, int logM, int32_t *d_idx, void *stream);
+/* y = x + sigma N(0, 1) [B][n] (sparc_sim.py:179-204) */
+int sg_awgn_device(int precision, uint64_t seed, uint64_t stream_id, const void *d_x, int B, int n, double sigma,
+                   void *d_y, void *stream);
+/* BPSK 1 - 2c over AWGN with variance sigma2, channel LLRs 2y/sigma2 [B][N] (ldpc_awgn.py:39-56) */
+int sg_bpsk_awgn_llr_device(int precision, uint64_t seed, uint64_t stream_id, const uint8_t *d_cw, int B, int N,
+                            double sigma2, void *d_llr, void *stream);
+/* Systematic LDPC encoder (ldpc.py:400-460) as a GF(2) product: parity
+ * [K][N-K] uint8 is the parity part of the code's generator (the encoder's
+ * image of the unit vectors); cw = [info, info P]. */
+typedef struct sg_ldpc_encoder sg_ldpc_encoder;
+int sg_ldpc_encoder_create(const uint8_t *parity, int K, int N, sg_ldpc_encoder **out);
+int sg_ldpc_encoder_destroy(sg_ldpc_encoder *e);
+int sg_ldpc_encode_device(sg_ldpc_encoder *e, const uint8_t *d_info, int B, uint8_t *d_cw, void *stream);
+
 /* ------------------------------------------------- integrated AMP <-> BP */
 /* The integrated decoders of sparc_sophie/sparc_new.py on a dense design
  * plan and an LDPC graph; every L log2 M bits of a codeword are LDPC
@@ -244,6 +267,9 @@ int sg_amp_decode_device(sg_amp_plan *p, const void *d_y, int B, const int32_t *
 /* Design operators (the Ab / Az closures of sparc_transforms, sparc.py:786-875):
  * transpose 0: in[B][L*M] -> out[B][n];  transpose 1: in[B][n] -> out[B][L*M]. */
 int sg_amp_apply(sg_amp_plan *p, int transpose, const double *in, int B, double *out);
+/* x = A beta0 [B][n] on the device for section indices d_idx [B][L]
+ * (one-hot beta0 with value 1, sparc.py:17-53 sparc_encode). */
+int sg_amp_encode_device(sg_amp_plan *p, const int32_t *d_idx, int B, void *d_x, void *stream);
 int sg_amp_apply_device(sg_amp_plan *p, int transpose, const void *d_in, int B, void *d_out,
                         void *stream);
 /* Adds {section errors, bit errors (popcount of index XOR, MSB-first bits as

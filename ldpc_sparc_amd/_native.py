@@ -100,6 +100,16 @@ SIGNATURES = [
                                                  ct.c_int, ct.c_int, ct.c_int, vp, vp]),
     ("sg_beta_to_llr_device", ct.c_int, [ct.c_int, vp, ct.c_int, ct.c_int, ct.c_int, ct.c_double, ct.c_int,
                                          ct.c_int, ct.c_int, ct.c_int, vp, vp]),
+    ("sg_amp_encode_device", ct.c_int, [vp, vp, ct.c_int, vp, vp]),
+    # device encoder and channel
+    ("sg_rng_bits_device", ct.c_int, [ct.c_uint64, ct.c_uint64, ct.c_int, ct.c_int, vp, vp]),
+    ("sg_bits_to_sections_device", ct.c_int, [vp, ct.c_int, ct.c_int, ct.c_int, vp, vp]),
+    ("sg_awgn_device", ct.c_int, [ct.c_int, ct.c_uint64, ct.c_uint64, vp, ct.c_int, ct.c_int, ct.c_double, vp, vp]),
+    ("sg_bpsk_awgn_llr_device", ct.c_int, [ct.c_int, ct.c_uint64, ct.c_uint64, vp, ct.c_int, ct.c_int, ct.c_double,
+                                           vp, vp]),
+    ("sg_ldpc_encoder_create", ct.c_int, [vp, ct.c_int, ct.c_int, vp]),
+    ("sg_ldpc_encoder_destroy", ct.c_int, [vp]),
+    ("sg_ldpc_encode_device", ct.c_int, [vp, vp, ct.c_int, vp, vp]),
     # integrated AMP <-> BP decoders
     ("sg_integrated_decode", ct.c_int, [vp, vp, ct.c_int, ct.c_int, vp, ct.c_int, ct.c_int, ct.c_int, ct.c_int,
                                         vp, vp]),
@@ -154,6 +164,11 @@ def require_gpu():
 
 def ptr(a):
     return ct.c_void_p(a.ctypes.data) if a is not None else ct.c_void_p(0)
+
+
+def offset(p, nbytes):
+    """Device pointer p (c_void_p) advanced by nbytes."""
+    return ct.c_void_p((p.value or 0) + int(nbytes))
 
 
 class DeviceBuffer:

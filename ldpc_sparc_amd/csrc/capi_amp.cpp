@@ -772,6 +772,41 @@ static int ensure_io(sg_amp_plan *p, size_t bytes) {
 
 using namespace sg;
 
+// One-hot message vectors (value 1, the public SPARC's beta0 before the
+// sqrt(W / L) scaling that the design applies, sparc.py:17-53) -> x = A beta0.
+template <typename T>
+__global__ void onehot_one_kernel(const int32_t *idx, int L, int M, T *beta) {
+    const int b = blockIdx.y;
+    for (int l = blockIdx.x * blockDim.x + threadIdx.x; l < L; l += gridDim.x * blockDim.x)
+        beta[(size_t)b * L * M + (size_t)l * M + idx[(size_t)b * L + l]] = T(1);
+}
+
+template <typename T>
+static int encode_impl(sg_amp_plan *p, const int32_t *d_idx, int B, T *d_x, hipStream_t s) {
+    SG_TRY(ensure_ws(p, B, 2));
+    T *beta0 = p->regular ? (T *)p->ws_s : (T *)p->ws_beta;
+    SG_HIP(hipMemsetAsync(beta0, 0, (size_t)B * p->LM * sizeof(T), s));
+    hipLaunchKernelGGL(onehot_one_kernel<T>, dim3((p->L + 255) / 256, B), dim3(256), 0, s, d_idx, p->L, p->M, beta0);
+    if (p->regular) {
+        RegTables<T> rt = rtables<T>(p);
+        RegBufs<T> rf = rbufs<T>(p, B, nullptr);
+        rf.mode = 1;
+        rf.ext_in = beta0;
+        rf.ext_out = d_x;
+        SG_TRY(reg_launch_ab<T>(rt, rf, s));
+        SG_TRY(reg_launch_ab_finish<T>(rt, rf, s));
+        return SG_OK;
+    }
+    AmpTables<T> tb = tables<T>(p);
+    AmpBufs<T> bf = bufs<T>(p, B, nullptr);
+    std::vector<int32_t> ones(B, 1);
+    SG_HIP(hipMemcpyAsync(p->ws_active, ones.data(), sizeof(int32_t) * B, hipMemcpyHostToDevice, s));
+    SG_TRY(amp_launch_ab<T>(tb, bf, s));
+    SG_TRY(amp_launch_rowsum<T>(tb, bf, d_x, s));
+    SG_HIP(hipStreamSynchronize(s));  // the host vector above
+    return SG_OK;
+}
+
 extern "C" {
 
 int sg_amp_plan_create(int ndim, const double *W, int Lr, int Lc, int L, int M, int n, const uint32_t *order0,
@@ -878,6 +913,15 @@ int sg_amp_apply(sg_amp_plan *p, int transpose, const double *in, int B, double 
     SG_HIP(hipMemcpyAsync(out, dout, nout * sizeof(double), hipMemcpyDeviceToHost, s));
     SG_HIP(hipStreamSynchronize(s));
     return SG_OK;
+}
+
+int sg_amp_encode_device(sg_amp_plan *p, const int32_t *d_idx, int B, void *d_x, void *stream) {
+    SG_CHECK_ARG(p && d_idx && d_x, "null argument");
+    if (B <= 0) return SG_OK;
+    SG_TRY(ensure_device());
+    hipStream_t s = pick_stream(stream);
+    return p->precision == SG_F64 ? encode_impl<double>(p, d_idx, B, (double *)d_x, s)
+                                  : encode_impl<float>(p, d_idx, B, (float *)d_x, s);
 }
 
 int sg_amp_apply_device(sg_amp_plan *p, int transpose, const void *d_in, int B, void *d_out, void *stream) {

@@ -9,6 +9,7 @@
 // f32 uses v_mfma_f32_32x32x2_f32 (exact f32 FMA chains); f64 (parity mode,
 // small designs) uses plain FMA kernels.
 #include "dense.hpp"
+#include "philox.hpp"
 
 namespace sg {
 
@@ -372,20 +373,6 @@ int concat_launch_count(const int32_t *map_idx, const int32_t *true_idx, int B, 
 // Throughput mode: A[i][j] ~ N(0, 1/n) from Philox4x32-10 (counter = element
 // index / 4, key = seed) and Box-Muller; statistically, not bitwise, equal to
 // numpy's default_rng(seed).normal (parity mode uploads the reference draw).
-__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
-        const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0, h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
-        c[0] = h1 ^ c[1] ^ k0;
-        c[1] = l1;
-        c[2] = h0 ^ c[3] ^ k1;
-        c[3] = l0;
-        k0 += 0x9E3779B9u;
-        k1 += 0xBB67AE85u;
-    }
-}
-
 template <typename T>
 __global__ void gen_A_kernel(T *A, long total, double scale, uint64_t seed) {
     const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;  // 4 outputs per thread

@@ -52,6 +52,7 @@ class code:
         self.K = self.Nv - self.Nc
         self._graph = None
         self._graph_dev = None
+        self._encoder = None
 
     # ------------------------------------------------------------ structure
     def assign_proto(self):
@@ -184,6 +185,34 @@ class code:
                 _native.lib().sg_ldpc_graph_destroy(g)
             except Exception:
                 pass
+        e = getattr(self, "_encoder", None)
+        if e is not None and e.value:
+            try:
+                _native.lib().sg_ldpc_encoder_destroy(e)
+            except Exception:
+                pass
+
+    # ------------------------------------------------------------ device encoder
+    def parity_generator(self):
+        """[K, N-K] uint8: the encoder's parity bits of every unit information
+        word (the encoder is GF(2)-linear and systematic, so cw = [u, u P])."""
+        cw = self.encode_batch(np.eye(self.K, dtype=np.int64))
+        assert np.array_equal(cw[:, :self.K], np.eye(self.K, dtype=int)), "encoder is not systematic"
+        return np.ascontiguousarray(cw[:, self.K:], dtype=np.uint8)
+
+    def _device_encoder(self):
+        _native.require_gpu()
+        if self._encoder is None:
+            P = self.parity_generator()
+            e = ct.c_void_p()
+            _native.check(_native.lib().sg_ldpc_encoder_create(_native.ptr(P), self.K, self.N, ct.byref(e)))
+            self._encoder = e
+        return self._encoder
+
+    def encode_device(self, d_info, B, d_cw, stream=None):
+        """Encode B information words already on the GPU (uint8 [B, K]) into
+        codewords (uint8 [B, N]) -- the throughput-mode encoder."""
+        _native.check(_native.lib().sg_ldpc_encode_device(self._device_encoder(), d_info, int(B), d_cw, stream))
 
     def decode(self, ch, max_itcount=200, dectype='sumprod2', corr_factor=0.7):
         """Decode one codeword of channel LLRs (ldpc.py:463-490) on the GPU in

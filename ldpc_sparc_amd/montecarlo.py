@@ -110,14 +110,39 @@ class LdpcTrial:
     decoded in batches on the GPU; counts over all N bits as the reference
     does (ldpc_awgn.py:97-104).  aux0 = sum of decode iteration counts."""
 
-    def __init__(self, c, snrs, dectype="sumprod2", max_it=200, corr=0.7, precision="f32", seed=0):
+    def __init__(self, c, snrs, dectype="sumprod2", max_it=200, corr=0.7, precision="f32", seed=0, rng="host"):
         self.c, self.snrs, self.dectype = c, list(snrs), dectype
         self.max_it, self.corr, self.seed = int(max_it), float(corr), int(seed)
         self.prec = {"f64": _native.SG_F64, "f32": _native.SG_F32}[precision]
+        if rng not in ("host", "device"):
+            raise ValueError("rng must be 'host' (numpy, reproducible against the reference's generators) "
+                             "or 'device' (Philox on the GPU, throughput mode)")
+        self.rng = rng
+
+    def _device_batch(self, point, first_block, n_blocks, block, sigma2):
+        """Information bits, encoding, BPSK and noise on the GPU; Philox stream
+        (point, block) so the draw does not depend on the rank or the batching."""
+        c, lib, off = self.c, _native.lib(), _native.offset
+        B = n_blocks * block
+        es = 8 if self.prec == _native.SG_F64 else 4
+        d_info = _native.DeviceBuffer(B * c.K)
+        d_x = _native.DeviceBuffer(B * c.N)
+        d_ch = _native.DeviceBuffer(B * c.N * es)
+        for i, blk in enumerate(range(first_block, first_block + n_blocks)):
+            sid = (int(point) << 32) | int(blk)
+            o = i * block
+            _native.check(lib.sg_rng_bits_device(self.seed, sid, block, c.K, off(d_info.ptr, o * c.K), None))
+            c.encode_device(off(d_info.ptr, o * c.K), block, off(d_x.ptr, o * c.N))
+            _native.check(lib.sg_bpsk_awgn_llr_device(self.prec, self.seed, sid, off(d_x.ptr, o * c.N), block, c.N,
+                                                      sigma2, off(d_ch.ptr, o * c.N * es), None))
+        return d_x, d_ch, B
 
     def __call__(self, point, first_block, n_blocks, block):
         c = self.c
         sigma2 = 1.0 / np.power(10, self.snrs[point] / 10.0)
+        if self.rng == "device":
+            d_x, d_ch, B = self._device_batch(point, first_block, n_blocks, block, sigma2)
+            return self._decode_count(d_x, d_ch, B)
         X, LLR = [], []
         for blk in range(first_block, first_block + n_blocks):
             rng = np.random.default_rng([self.seed, point, blk])
@@ -129,12 +154,16 @@ class LdpcTrial:
         LLR = np.concatenate(LLR)
         B = X.shape[0]
         dt = np.float64 if self.prec == _native.SG_F64 else np.float32
-        lib = _native.lib()
-        g = c._device_graph()
         d_ch = _native.DeviceBuffer.from_array(LLR.astype(dt))
+        d_x = _native.DeviceBuffer.from_array(X.astype(np.uint8))
+        return self._decode_count(d_x, d_ch, B)
+
+    def _decode_count(self, d_x, d_ch, B):
+        c, lib = self.c, _native.lib()
+        dt = np.float64 if self.prec == _native.SG_F64 else np.float32
+        g = c._device_graph()
         d_app = _native.DeviceBuffer(B * c.N * np.dtype(dt).itemsize)
         d_it = _native.DeviceBuffer(B * 4)
-        d_x = _native.DeviceBuffer.from_array(X.astype(np.uint8))
         d_cnt = _native.DeviceBuffer(32)
         d_cnt.zero()
         _native.check(lib.sg_ldpc_decode_device(g, _native.DECTYPES[self.dectype], self.prec, d_ch.ptr, B,
@@ -144,6 +173,55 @@ class LdpcTrial:
         _native.synchronize()
         cnt = d_cnt.download(np.zeros(4, np.int64))
         return np.array([B, cnt[0], cnt[1], cnt[3], 0], dtype=np.int64)
+
+
+class SparcTrial:
+    """Regular SPARC with the sub-sampled DCT design over AWGN, generated and
+    decoded on the GPU (throughput mode): Philox bits ->
+    section indices -> x = A beta0 (sparc.py:17-53) -> y = x + N(0, awgn_var)
+    (sparc_sim.py:179-204) -> AMP (sparc.py:883-999) -> errors.  Counters
+    [codewords, bit errors, codeword errors, AMP iterations, section errors];
+    the Philox stream of block b at point p is (p, b), so results do not
+    depend on the rank count.  op: sparc.DesignOperator (shared design)."""
+
+    def __init__(self, op, awgn_vars, t_max=25, rtol=1e-6, phi_method=1, precision="f32", seed=0):
+        self.op, self.vars = op, list(awgn_vars)
+        self.t_max, self.rtol, self.phi = int(t_max), float(rtol), int(phi_method)
+        self.prec = {"f64": _native.SG_F64, "f32": _native.SG_F32}[precision]
+        self.seed = int(seed)
+        self.logM = int(np.log2(op.M))
+
+    def __call__(self, point, first_block, n_blocks, block):
+        op, lib, off = self.op, _native.lib(), _native.offset
+        L, n, logM = op.L, op.n, self.logM
+        es = 8 if self.prec == _native.SG_F64 else 4
+        B = n_blocks * block
+        plan = op.plan(self.prec)
+        d_bits = _native.DeviceBuffer(B * L * logM)
+        d_true = _native.DeviceBuffer(B * L * 4)
+        d_x = _native.DeviceBuffer(B * n * es)
+        d_y = _native.DeviceBuffer(B * n * es)
+        sigma = float(np.sqrt(self.vars[point]))
+        for i, blk in enumerate(range(first_block, first_block + n_blocks)):
+            sid = (int(point) << 32) | int(blk)
+            o = i * block
+            _native.check(lib.sg_rng_bits_device(self.seed, sid, block, L * logM, off(d_bits.ptr, o * L * logM), None))
+        _native.check(lib.sg_bits_to_sections_device(d_bits.ptr, B, L, logM, d_true.ptr, None))
+        _native.check(lib.sg_amp_encode_device(plan, d_true.ptr, B, d_x.ptr, None))
+        for i, blk in enumerate(range(first_block, first_block + n_blocks)):
+            sid = (int(point) << 32) | int(blk)
+            o = i * block
+            _native.check(lib.sg_awgn_device(self.prec, self.seed, sid, off(d_x.ptr, o * n * es), block, n, sigma,
+                                             off(d_y.ptr, o * n * es), None))
+        d_map = _native.DeviceBuffer(B * L * 4)
+        d_tf = _native.DeviceBuffer(B * 4)
+        d_cnt = _native.DeviceBuffer(4 * 8)
+        d_cnt.zero()
+        _native.check(lib.sg_amp_decode_device(plan, d_y.ptr, B, d_true.ptr, float(self.vars[point]), self.t_max,
+                                               self.rtol, self.phi, d_map.ptr, d_tf.ptr, None, None, None))
+        _native.check(lib.sg_amp_count_errors_device(d_map.ptr, d_true.ptr, d_tf.ptr, B, L, logM, d_cnt.ptr, None))
+        cnt = d_cnt.download(np.zeros(4, np.int64))
+        return np.array([B, cnt[1], cnt[2], cnt[3], cnt[0]], dtype=np.int64)
 
 
 def ldpc_awgn_campaign(standard, rate, z, ptype="A", *, rank=0, world=1, agg=None, N_MEASUREMENTS=24,
