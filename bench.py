@@ -39,6 +39,7 @@ from ldpc_sparc_amd.ldpc import code  # noqa: E402
 
 METRIC = "codewords/sec (AMP+BP) at L=1024 M=512 / n=1944; BER match vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+VALU_PEAK_TFS = 157.3  # MI355X f32 vector peak (packed FMA), MI355X_MICROARCH.md
 AMP_PHASES = ("ab_passA", "ab_passB", "az_passA", "az_passB", "eta", "control")
 
 
@@ -61,6 +62,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="approximate CPU-baseline sample length (0 disables)")
     ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
+    ap.add_argument("--seed", type=int, default=1, help="Philox key of the synthetic inputs (stream = rank)")
     return ap.parse_args()
 
 
@@ -115,20 +117,23 @@ def amp_setup(args, rank):
     op = sparc.DesignOperator(W, L, M, n, o0, o1)
     plan = op.plan(prec)
     B = args.batch
-    rng = np.random.default_rng(1000 + rank)
-    true = rng.integers(0, M, (B, L)).astype(np.int32)
-    # encode x = A beta0 on the GPU (sparc.py:51), add AWGN (sparc_sim.py:179-204)
-    beta0 = np.zeros((B, L * M))
-    beta0[np.arange(B)[:, None], np.arange(L) * M + true] = 1.0
-    X = op.apply(beta0, False, _native.SG_F64)
-    del beta0
-    Y = X + rng.standard_normal((B, n))
-    dt = np.float32 if prec == _native.SG_F32 else np.float64
-    st = dict(L=L, M=M, logM=logM, n=n, B=B, op=op, plan=plan, prec=prec,
-              d_y=_native.DeviceBuffer.from_array(Y.astype(dt)),
-              d_true=_native.DeviceBuffer.from_array(true),
+    # throughput-mode input: Philox bits keyed by the rank
+    # -> section indices -> x = A beta0 (sparc.py:51) -> AWGN, all on the GPU
+    lib = _native.lib()
+    es = 4 if prec == _native.SG_F32 else 8
+    d_bits = _native.DeviceBuffer(B * L * logM)
+    d_true = _native.DeviceBuffer(B * L * 4)
+    d_x = _native.DeviceBuffer(B * n * es)
+    d_y = _native.DeviceBuffer(B * n * es)
+    _native.check(lib.sg_rng_bits_device(args.seed, rank, B, L * logM, d_bits.ptr, None))
+    _native.check(lib.sg_bits_to_sections_device(d_bits.ptr, B, L, logM, d_true.ptr, None))
+    _native.check(lib.sg_amp_encode_device(plan, d_true.ptr, B, d_x.ptr, None))
+    _native.check(lib.sg_awgn_device(prec, args.seed, rank, d_x.ptr, B, n, 1.0, d_y.ptr, None))
+    _native.synchronize()
+    del d_bits, d_x
+    st = dict(L=L, M=M, logM=logM, n=n, B=B, op=op, plan=plan, prec=prec, d_y=d_y, d_true=d_true,
               d_map=_native.DeviceBuffer(B * L * 4), d_tf=_native.DeviceBuffer(B * 4),
-              d_cnt=_native.DeviceBuffer(4 * 8), W=W, o0=o0, o1=o1, Y=Y, true=true)
+              d_cnt=_native.DeviceBuffer(4 * 8), W=W, o0=o0, o1=o1)
     return st
 
 
@@ -150,13 +155,17 @@ def amp_cpu_baseline(st, args, seconds):
     from oracle import sparc_ref
     L, M, n = st["L"], st["M"], st["n"]
     Ab, Az = sparc_ref.dct_operators(st["W"], L, M, n, st["o0"], st["o1"])
+    # the same received words and message indices the GPU decodes
+    dt = np.float32 if st["prec"] == _native.SG_F32 else np.float64
+    Y = st["d_y"].download(np.zeros((st["B"], n), dt)).astype(np.float64)
+    true = st["d_true"].download(np.zeros((st["B"], L), np.int32))
     t0 = time.perf_counter()
     done = iters = 0
     while True:
         b = done
         beta0 = np.zeros(L * M)
-        beta0[np.arange(L) * M + st["true"][b]] = 1.0
-        _, tf, _, _ = sparc_ref.amp(st["Y"][b], st["W"], L, M, n, 1.0, args.t_max, Ab, Az, beta0)
+        beta0[np.arange(L) * M + true[b]] = 1.0
+        _, tf, _, _ = sparc_ref.amp(Y[b], st["W"], L, M, n, 1.0, args.t_max, Ab, Az, beta0)
         done += 1
         iters += tf
         el = time.perf_counter() - t0
@@ -294,6 +303,8 @@ def main():
     cw_it = int(tf.sum()) * args.steps  # executed codeword-iterations on this rank
     amp_ms = sum(phases.get(p, (0.0, 0))[0] for p in AMP_PHASES)
     bytes_per_cwit = 4 * (2 * st["L"] * st["M"] + 4 * st["n"])
+    w = int(st["op"].w)  # transform length (2^20 at C2)
+    flops_per_cwit = 2 * 2.5 * w * np.log2(w) + 20 * st["L"] * st["M"]
     achieved = bytes_per_cwit * cw_it / (amp_ms * 1e-3) / 1e9 if amp_ms > 0 else None
     total_cw = d.world * st["B"] * args.steps
     traffic = None
@@ -313,8 +324,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32" if st["prec"] == _native.SG_F32 else "f64",
-        "data": "synthetic: random messages, encoded x = A beta0 with the benchmark design, AWGN "
-                "sigma^2=1 (host numpy RNG), resident in HBM before timing",
+        "data": "synthetic: Philox random messages (stream = rank), encoded x = A beta0 with the benchmark "
+                "design and AWGN sigma^2=1 on the GPU (throughput mode), resident in HBM before timing",
         "config": {"workload": "C2: SPARC AMP, regular design, sub-sampled DCT operator w=2^20",
                    "L": st["L"], "M": st["M"], "n": st["n"], "R": args.rate, "P": 15.0,
                    "awgn_var": 1.0, "t_max": args.t_max, "batch_per_gpu": st["B"],
@@ -329,6 +340,13 @@ def main():
                      "codeword_iterations": cw_it,
                      "kernel_ms": {k: round(v[0], 3) for k, v in phases.items()},
                      "launches": {k: v[1] for k, v in phases.items()}},
+        "roofline_flops": {"bound": "valu-f32", "achieved": flops_per_cwit * cw_it / (amp_ms * 1e-3) / 1e12
+                           if amp_ms > 0 else None, "peak": VALU_PEAK_TFS, "unit": "TFLOP/s",
+                           "frac": flops_per_cwit * cw_it / (amp_ms * 1e-3) / 1e12 / VALU_PEAK_TFS
+                           if amp_ms > 0 else None,
+                           "algorithmic_flops_per_codeword_iteration": flops_per_cwit,
+                           "note": "SURVEY.md 8(d): 2 transforms x 2.5 w log2 w + 20 L M; the FFTs run on the "
+                                   "vector ALUs (packed f32), so the f32 vector peak applies"},
         "amp": {"avg_iterations": float(tf.mean()), "section_errors": int(cnt[0]),
                 "bit_errors": int(cnt[1]), "codeword_errors": int(cnt[2]),
                 "ber": float(cnt[1]) / (d.world * st["B"] * st["L"] * st["logM"])},
