@@ -191,6 +191,16 @@ int sg_ldpc_encoder_create(const uint8_t *parity, int K, int N, sg_ldpc_encoder 
 int sg_ldpc_encoder_destroy(sg_ldpc_encoder *e);
 int sg_ldpc_encode_device(sg_ldpc_encoder *e, const uint8_t *d_info, int B, uint8_t *d_cw, void *stream);
 
+/* ------------------------------------------------------ state evolution */
+/* SPARC state evolution (sparc_public/sparc_se.py:82-183): Monte-Carlo samples
+ * u [mc][M] (the reference's np.random.randn draw) stay on the device;
+ * sg_se_expectation evaluates sparc_se_E (:82-115) for nt values of tau at
+ * once (K = 1, or K = 2 for real modulated SPARCs). */
+typedef struct sg_se_samples sg_se_samples;
+int sg_se_samples_create(const double *u, int mc, int M, sg_se_samples **out);
+int sg_se_samples_destroy(sg_se_samples *h);
+int sg_se_expectation(sg_se_samples *h, int K, const double *taus, int nt, double *E);
+
 /* ------------------------------------------------- integrated AMP <-> BP */
 /* The integrated decoders of sparc_sophie/sparc_new.py on a dense design
  * plan and an LDPC graph; every L log2 M bits of a codeword are LDPC

@@ -110,6 +110,10 @@ SIGNATURES = [
     ("sg_ldpc_encoder_create", ct.c_int, [vp, ct.c_int, ct.c_int, vp]),
     ("sg_ldpc_encoder_destroy", ct.c_int, [vp]),
     ("sg_ldpc_encode_device", ct.c_int, [vp, vp, ct.c_int, vp, vp]),
+    # state evolution
+    ("sg_se_samples_create", ct.c_int, [vp, ct.c_int, ct.c_int, vp]),
+    ("sg_se_samples_destroy", ct.c_int, [vp]),
+    ("sg_se_expectation", ct.c_int, [vp, ct.c_int, vp, ct.c_int, vp]),
     # integrated AMP <-> BP decoders
     ("sg_integrated_decode", ct.c_int, [vp, vp, ct.c_int, ct.c_int, vp, ct.c_int, ct.c_int, ct.c_int, ct.c_int,
                                         vp, vp]),

@@ -46,3 +46,9 @@ def sophie_golden():
 def integrated_golden():
     import numpy as np
     return np.load(os.path.join(REPO, "tests", "golden", "integrated_golden.npz"))
+
+
+@pytest.fixture(scope="session")
+def se_golden():
+    import numpy as np
+    return np.load(os.path.join(REPO, "tests", "golden", "se_golden.npz"))
