@@ -53,6 +53,9 @@ int sg_memcpy_h2d(void *dst, const void *src, size_t bytes, void *stream);
 int sg_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream);
 int sg_memset(void *dptr, int value, size_t bytes, void *stream);
 int sg_stream_synchronize(void *stream);
+/* An extra non-blocking stream (concurrent batches on one GPU). */
+int sg_stream_create(void **stream);
+int sg_stream_destroy(void *stream);
 
 /* HIP events on a given stream (bench.py times the kernels on the stream they
  * run on, not on torch's current stream). */

@@ -45,6 +45,8 @@ SIGNATURES = [
     ("sg_memcpy_h2d", ct.c_int, [vp, vp, ct.c_size_t, vp]),
     ("sg_memcpy_d2h", ct.c_int, [vp, vp, ct.c_size_t, vp]),
     ("sg_memset", ct.c_int, [vp, ct.c_int, ct.c_size_t, vp]),
+    ("sg_stream_create", ct.c_int, [vp]),
+    ("sg_stream_destroy", ct.c_int, [vp]),
     ("sg_stream_synchronize", ct.c_int, [vp]),
     ("sg_event_create", ct.c_int, [ct.POINTER(vp)]),
     ("sg_event_destroy", ct.c_int, [vp]),

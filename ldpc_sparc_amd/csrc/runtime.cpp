@@ -191,6 +191,20 @@ int sg_stream_synchronize(void *stream) {
     return SG_OK;
 }
 
+int sg_stream_create(void **stream) {
+    SG_CHECK_ARG(stream, "null argument");
+    SG_TRY(ensure_device());
+    hipStream_t s = nullptr;
+    SG_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *stream = s;
+    return SG_OK;
+}
+
+int sg_stream_destroy(void *stream) {
+    if (stream) SG_HIP(hipStreamDestroy((hipStream_t)stream));
+    return SG_OK;
+}
+
 int sg_profile_enable(int on) {
     std::lock_guard<std::mutex> lk(g_mu);
     g_prof_on = on != 0;
