@@ -100,6 +100,7 @@ struct RegTables {
     int nB;                   // ceil(P / 64)
     int ept;                  // stage-1 FFT elements per thread (block = P / ept)
     int maxcls;               // largest class (entries of one m2 within a column block)
+    int img;                  // reals of the stage-1 LDS image: max(2P, fpad(maxcls + 16))
     int skip;                 // timing ablation only (SG_AMP_SKIP): 1 FFT, 2 gather/scatter, 4 row I/O
 };
 
@@ -136,7 +137,7 @@ template <typename T>
 int reg_launch_map(const RegTables<T> &tb, const RegBufs<T> &bf, hipStream_t s);
 template <typename T>
 int reg_launch_ab_finish(const RegTables<T> &tb, const RegBufs<T> &bf, hipStream_t s);
-size_t reg_stage1_lds(int P, int Lblk, size_t real_bytes);
+size_t reg_stage1_lds(int img, int P, int Lblk, size_t real_bytes);
 // stage-1 elements per thread: f32 at P >= 8192 uses 16 (P = 8192 -> 512-thread
 // workgroups, two per CU); otherwise P/1024 threads' worth, at least 8
 inline int reg_ept(int P, size_t real_bytes) {

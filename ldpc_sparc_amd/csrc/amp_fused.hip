@@ -72,9 +72,10 @@ constexpr int REG_CH = 8;  // entries a thread loads before using them
 // block size of a stage-1 kernel: P / EPT for the compile-time sizes
 constexpr int reg_s1_threads(int EPT, int LOG2P) { return LOG2P > 0 ? (1 << LOG2P) / EPT : 1024; }
 
-size_t reg_stage1_lds(int P, int Lblk, size_t real_bytes) {
-    return (size_t)(P + (P >> 4)) * 2 * real_bytes + (size_t)2 * Lblk * real_bytes +
-           (size_t)(64 + (P + 63) / 64) * 2 * real_bytes;
+// LDS of a stage-1 workgroup: the FFT / class image (img reals), the section
+// statistics, the class twiddles
+size_t reg_stage1_lds(int img, int P, int Lblk, size_t real_bytes) {
+    return (size_t)img * real_bytes + (size_t)2 * Lblk * real_bytes + (size_t)(64 + (P + 63) / 64) * 2 * real_bytes;
 }
 
 // ------------------------------------------------------------------ ab stage 1
@@ -83,8 +84,7 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_ab_stage1(RegT
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     cx<T> *d = reinterpret_cast<cx<T> *>(smem);
     T *dr = reinterpret_cast<T *>(smem);
-    const int Pp = tb.P + (tb.P >> 4);  // FFT image (fsw) and the skewed class image (fpad)
-    T *sM = dr + 2 * (size_t)Pp;
+    T *sM = dr + tb.img;  // after the FFT image (fsw) / skewed class image (fpad)
     T *sI = sM + tb.Lblk;
     cx<T> *ta = reinterpret_cast<cx<T> *>(sI + tb.Lblk);  // w_N2^(m2 k1) factors of this class
     cx<T> *tbb = ta + 64;
@@ -297,8 +297,7 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_az_stage2(RegT
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     cx<T> *d = reinterpret_cast<cx<T> *>(smem);
     T *dr = reinterpret_cast<T *>(smem);
-    const int Pp = tb.P + (tb.P >> 4);  // FFT image (fsw) and the skewed class image (fpad)
-    T *sM = dr + 2 * (size_t)Pp;
+    T *sM = dr + tb.img;  // after the FFT image (fsw) / skewed class image (fpad)
     T *sI = sM + tb.Lblk;
     const int m2 = blockIdx.x, t = blockIdx.y, cw = blockIdx.z;
     if (bf.mode == 0 && !bf.active[cw] && !tb.skip) return;
@@ -658,6 +657,7 @@ static void launch_s2i(const RegTables<T> &tb, const RegBufs<T> &bf, int t_iter,
 // compile-time FFT for the benchmark sizes (f32: P = 2^14 at EPT 16; f64:
 // P = 2^13 at EPT 8)
 constexpr int reg_hot_log2p(bool dbl) { return dbl ? 13 : 14; }
+constexpr int reg_hot2_log2p(bool dbl) { return 13; }  // f32 at P = 2^13 (SG_AMP_PMAX=8192: two workgroups per CU)
 
 template <typename T>
 static int reg_set_attrs() {
@@ -669,6 +669,10 @@ static int reg_set_attrs() {
     SG_LDS_ATTR((reg_ab_stage1<T, 8, 0>)); SG_LDS_ATTR((reg_ab_stage1<T, 16, 0>));
     SG_LDS_ATTR((reg_az_stage2<T, 8, 0>)); SG_LDS_ATTR((reg_az_stage2<T, 16, 0>));
     SG_LDS_ATTR((reg_ab_stage1<T, HE, H>)); SG_LDS_ATTR((reg_az_stage2<T, HE, H>));
+    if constexpr (sizeof(T) == 4) {
+        constexpr int H2 = reg_hot2_log2p(false);
+        SG_LDS_ATTR((reg_ab_stage1<T, HE, H2>)); SG_LDS_ATTR((reg_az_stage2<T, HE, H2>));
+    }
     SG_LDS_ATTR((reg_ab_stage2<T>)); SG_LDS_ATTR((reg_az_stage1<T>));
 #undef SG_LDS_ATTR
     done = true;
@@ -679,12 +683,14 @@ template <typename T>
 int reg_launch_ab(const RegTables<T> &tb, const RegBufs<T> &bf, hipStream_t s) {
     if (bf.B <= 0) return SG_OK;
     SG_TRY(reg_set_attrs<T>());
-    const size_t lds1 = reg_stage1_lds(tb.P, tb.Lblk, sizeof(T));
+    const size_t lds1 = reg_stage1_lds(tb.img, tb.P, tb.Lblk, sizeof(T));
     const int ept = tb.ept;
     {
         ProfScope ps(SG_PH_AB_A, s);
         constexpr int H = reg_hot_log2p(sizeof(T) == 8), HE = sizeof(T) == 8 ? 8 : 16;
         if (tb.log2P == H && ept == HE) launch_s1<T, HE, H>(tb, bf, lds1, s);
+        else if (sizeof(T) == 4 && tb.log2P == reg_hot2_log2p(false) && ept == HE)
+            launch_s1<T, HE, reg_hot2_log2p(false)>(tb, bf, lds1, s);
         else if (ept == 8) launch_s1<T, 8, 0>(tb, bf, lds1, s);
         else if (ept == 16) launch_s1<T, 16, 0>(tb, bf, lds1, s);
         else return fail(SG_ERR_UNSUPPORTED, "stage-1 FFT length P=%d unsupported", tb.P);
@@ -717,12 +723,14 @@ int reg_launch_az(const RegTables<T> &tb, const RegBufs<T> &bf, int t_iter, hipS
         hipLaunchKernelGGL((reg_az_stage1<T>), dim3(tb.nrb, tb.nT, bf.B), dim3(256), ldsg, s, tb, bf);
     }
     SG_HIP(hipGetLastError());
-    const size_t lds1 = reg_stage1_lds(tb.P, tb.Lblk, sizeof(T));
+    const size_t lds1 = reg_stage1_lds(tb.img, tb.P, tb.Lblk, sizeof(T));
     const int ept = tb.ept;
     {
         ProfScope ps(SG_PH_AZ_B, s);
         constexpr int H = reg_hot_log2p(sizeof(T) == 8), HE = sizeof(T) == 8 ? 8 : 16;
         if (tb.log2P == H && ept == HE) launch_s2i<T, HE, H>(tb, bf, t_iter, lds1, s);
+        else if (sizeof(T) == 4 && tb.log2P == reg_hot2_log2p(false) && ept == HE)
+            launch_s2i<T, HE, reg_hot2_log2p(false)>(tb, bf, t_iter, lds1, s);
         else if (ept == 8) launch_s2i<T, 8, 0>(tb, bf, t_iter, lds1, s);
         else if (ept == 16) launch_s2i<T, 16, 0>(tb, bf, t_iter, lds1, s);
         else return fail(SG_ERR_UNSUPPORTED, "stage-1 FFT length P=%d unsupported", tb.P);

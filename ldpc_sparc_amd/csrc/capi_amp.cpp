@@ -37,7 +37,7 @@ struct sg_amp_plan {
     int32_t *ws_active = nullptr, *ws_argmax = nullptr, *ws_true = nullptr, *ws_tfinal = nullptr;
     // regular engine (one transform per column block, amp_fused.hip)
     bool regular = false;
-    int rP = 0, rQ = 0, rlog2P = 0, rept = 0, rmaxcls = 0, nRmax = 0, nKmax = 0, RB = 0, nrb = 0, maxKb = 0, Lblk = 0, nB = 0;
+    int rP = 0, rQ = 0, rlog2P = 0, rept = 0, rmaxcls = 0, rimg = 0, nRmax = 0, nKmax = 0, RB = 0, nrb = 0, maxKb = 0, Lblk = 0, nB = 0;
     int32_t *r_nR = nullptr, *r_row_k1 = nullptr, *r_kptr = nullptr, *r_kk2 = nullptr, *r_krho = nullptr;
     int32_t *r_oa = nullptr, *r_ob = nullptr, *r_gi = nullptr, *r_cls_ptr = nullptr, *r_cls_j = nullptr,
             *r_qpos = nullptr;
@@ -232,8 +232,9 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
     long long Pmax = p->precision == SG_F64 ? 8192 : 16384;
     if (const char *e = getenv("SG_AMP_PMAX")) Pmax = std::max(8LL, std::min(Pmax, atoll(e)));  // tuning knob
     int P = (int)std::min<long long>(N2, Pmax);
-    while (P > 8 && reg_stage1_lds(P, Lblk, rb) > 160 * 1024) P >>= 1;
-    SG_CHECK_ARG(reg_stage1_lds(P, Lblk, rb) <= 160 * 1024, "section statistics exceed the LDS budget");
+    auto img_bound = [](int P) { return 2 * (P + (P >> 4)); };  // before the classes are known
+    while (P > 8 && reg_stage1_lds(img_bound(P), P, Lblk, rb) > 160 * 1024) P >>= 1;
+    SG_CHECK_ARG(reg_stage1_lds(img_bound(P), P, Lblk, rb) <= 160 * 1024, "section statistics exceed the LDS budget");
     const int Q = (int)(N2 / P);
     p->rP = P; p->rQ = Q; p->rlog2P = ilog2(P); p->Lblk = Lblk;
     p->rept = reg_ept(P, rb);
@@ -412,6 +413,8 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
     for (int t = 0; t < nT; ++t)
         for (int m2 = 0; m2 < Q; ++m2)
             p->rmaxcls = std::max(p->rmaxcls, cls_ptr[(size_t)t * (Q + 1) + m2 + 1] - cls_ptr[(size_t)t * (Q + 1) + m2]);
+    p->rimg = (std::max(2 * P, fpad(p->rmaxcls + 16) + 1) + 3) / 4 * 4;
+    SG_CHECK_ARG(reg_stage1_lds(p->rimg, P, Lblk, rb) <= 160 * 1024, "a class exceeds the LDS budget");
     SG_TRY(upload(p, &p->r_cls_ptr, cls_ptr));
     SG_TRY(upload(p, &p->r_cls_ls, cls_ls));
     SG_TRY(upload(p, &p->r_cls_j, cls_j));
@@ -429,7 +432,7 @@ template <typename T>
 static RegTables<T> rtables(const sg_amp_plan *p) {
     RegTables<T> tb;
     tb.nT = p->nT; tb.L = p->L; tb.M = p->M; tb.LM = p->LM; tb.n = p->n; tb.Lc = p->Lc; tb.Mc = p->Mc;
-    tb.Lblk = p->Lblk; tb.N2 = p->N2; tb.P = p->rP; tb.Q = p->rQ; tb.log2P = p->rlog2P; tb.ept = p->rept; tb.maxcls = p->rmaxcls;
+    tb.Lblk = p->Lblk; tb.N2 = p->N2; tb.P = p->rP; tb.Q = p->rQ; tb.log2P = p->rlog2P; tb.ept = p->rept; tb.maxcls = p->rmaxcls; tb.img = p->rimg;
     tb.nRmax = p->nRmax; tb.nKmax = p->nKmax; tb.RB = p->RB; tb.nrb = p->nrb; tb.maxKb = p->maxKb;
     tb.nR = p->r_nR; tb.row_k1 = p->r_row_k1; tb.kptr = p->r_kptr; tb.kk2 = p->r_kk2; tb.krho = p->r_krho;
     tb.oa = p->r_oa; tb.ob = p->r_ob; tb.oc = (const cx<T> *)p->r_oc; tb.gi = p->r_gi; tb.gc = (const cx<T> *)p->r_gc;
