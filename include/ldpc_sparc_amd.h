@@ -283,6 +283,11 @@ int sg_amp_apply(sg_amp_plan *p, int transpose, const double *in, int B, double 
 /* x = A beta0 [B][n] on the device for section indices d_idx [B][L]
  * (one-hot beta0 with value 1, sparc.py:17-53 sparc_encode). */
 int sg_amp_encode_device(sg_amp_plan *p, const int32_t *d_idx, int B, void *d_x, void *stream);
+/* Diagnostics: mean shader-clock cycles of the phases of the last stage-1
+ * launches (kernel 0 = Ab stage 1, 1 = Az stage 2; mean_cycles[8], entry k =
+ * timestamp k minus timestamp k-1).  Only with SG_AMP_TPROF set in the
+ * environment; otherwise *nphases = 0. */
+int sg_amp_stage_profile(sg_amp_plan *p, int kernel, double *mean_cycles, int *nphases);
 int sg_amp_apply_device(sg_amp_plan *p, int transpose, const void *d_in, int B, void *d_out,
                         void *stream);
 /* Adds {section errors, bit errors (popcount of index XOR, MSB-first bits as

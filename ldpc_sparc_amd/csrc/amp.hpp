@@ -121,6 +121,7 @@ struct RegBufs {
     int32_t *map;           // [B][L]
     const T *ext_in;        // mode 1: [B][LM] (Ab) or [B][n] (Az)
     T *ext_out;             // mode 1: [B][n] (Ab) or [B][LM] (Az)
+    uint64_t *tprof_ab, *tprof_az;  // diagnostics (SG_AMP_TPROF): [B][nT][Q][8] phase timestamps, or null
 };
 
 template <typename T>

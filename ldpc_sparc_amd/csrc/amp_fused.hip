@@ -67,6 +67,12 @@ __device__ __forceinline__ double reg_block_sum(double v, double *red) {
     return t;
 }
 
+// diagnostics: wave 0 of a workgroup stamps the shader clock at phase k
+#define SG_TP(buf, k)                                                                                           \
+    do {                                                                                                        \
+        if ((buf) && tid == 0) (buf)[(((size_t)cw * tb.nT + t) * tb.Q + m2) * 8 + (k)] = __builtin_readcyclecounter(); \
+    } while (0)
+
 constexpr int REG_CH = 8;  // entries a thread loads before using them
 
 // block size of a stage-1 kernel: P / EPT for the compile-time sizes
@@ -91,6 +97,7 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_ab_stage1(RegT
     const int m2 = blockIdx.x, t = blockIdx.y, cw = blockIdx.z;
     if (bf.mode == 0 && !bf.active[cw] && !tb.skip) return;
     const int tid = threadIdx.x, nthr = blockDim.x;
+    SG_TP(bf.tprof_ab, 0);
     if (!(tb.skip & 16))
         for (int i = tid; i < tb.P * (int)sizeof(cx<T>) / 16; i += nthr) reinterpret_cast<uint4 *>(smem)[i] = uint4{0, 0, 0, 0};
     for (int i = tid; i < 64 + tb.nB; i += nthr)
@@ -108,6 +115,7 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_ab_stage1(RegT
         inv_tau = (T)(1.0 / tv);
     }
     __syncthreads();
+    SG_TP(bf.tprof_ab, 1);
     const int32_t *cp = tb.cls_ptr + (size_t)t * (tb.Q + 1);
     const int q0 = cp[m2], q1 = cp[m2 + 1];
     const uint32_t *ls = tb.cls_ls + tc;
@@ -137,10 +145,12 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_ab_stage1(RegT
         for (int q = q0 + tid; q < q1; q += nthr) dr[ls[q] & 0xffffu] = x[cj[q]];
     }
     __syncthreads();
+    SG_TP(bf.tprof_ab, 2);
     if (!(tb.skip & 1)) {
         if constexpr (LOG2P > 0) lds_fft1_ct<T, false, EPT, LOG2P>(d, tb.stw, tid);
         else lds_fft1<T, false, EPT>(d, tb.log2P, tb.stw, tid, nthr);
     }
+    SG_TP(bf.tprof_ab, 3);
     const int nR = (tb.skip & 4) ? 0 : tb.nR[t];
     const int32_t *rk = tb.row_k1 + (size_t)t * tb.nRmax;
     cx<T> *out = bf.tu + (((size_t)cw * tb.nT + t) * tb.Q + m2) * tb.nRmax;
@@ -155,6 +165,9 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_ab_stage1(RegT
     for (int i = 0; i < EPT; ++i) {
         const int r = tid + i * nthr;
         if (r < nR) out[r] = cmul(d[fsw(k1[i])], cmul(ta[k1[i] & 63], tbb[k1[i] >> 6]));
+    }
+    if (bf.tprof_ab) {
+        SG_TP(bf.tprof_ab, 4); SG_TP(bf.tprof_ab, 5); SG_TP(bf.tprof_ab, 6); SG_TP(bf.tprof_ab, 7);
     }
 }
 
@@ -302,6 +315,7 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_az_stage2(RegT
     const int m2 = blockIdx.x, t = blockIdx.y, cw = blockIdx.z;
     if (bf.mode == 0 && !bf.active[cw] && !tb.skip) return;
     const int tid = threadIdx.x, nthr = blockDim.x;
+    SG_TP(bf.tprof_az, 0);
     if (!(tb.skip & 16))
         for (int i = tid; i < tb.P * (int)sizeof(cx<T>) / 16; i += nthr) reinterpret_cast<uint4 *>(smem)[i] = uint4{0, 0, 0, 0};
     T tp = T(1), inv_tp = T(1);
@@ -317,6 +331,7 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_az_stage2(RegT
         inv_tp = (T)(1.0 / tv);
     }
     __syncthreads();
+    SG_TP(bf.tprof_az, 1);
     const int nR = (tb.skip & 4) ? 0 : tb.nR[t];
     const int32_t *rk = tb.row_k1 + (size_t)t * tb.nRmax;
     const cx<T> *src = bf.tu + (((size_t)cw * tb.nT + t) * tb.Q + m2) * tb.nRmax;
@@ -336,10 +351,12 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_az_stage2(RegT
             if (base + i * nthr < nR) d[fsw(k1[i])] = v[i];
     }
     __syncthreads();
+    SG_TP(bf.tprof_az, 2);
     if (!(tb.skip & 1)) {
         if constexpr (LOG2P > 0) lds_fft1_ct<T, true, EPT, LOG2P>(d, tb.stw, tid);
         else lds_fft1<T, true, EPT>(d, tb.log2P, tb.stw, tid, nthr);
     }
+    SG_TP(bf.tprof_az, 3);
     const size_t tc = (size_t)t * tb.Mc;
     const int32_t *cp = tb.cls_ptr + (size_t)t * (tb.Q + 1);
     const int q0 = cp[m2], q1 = cp[m2 + 1];
@@ -380,6 +397,7 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_az_stage2(RegT
             }
         }
     }
+    SG_TP(bf.tprof_az, 4);
     __syncthreads();
 #pragma unroll
     for (int c = 0; c < 2 * EPT; ++c) {  // s of the class in class order, skewed by fpad
@@ -387,6 +405,7 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_az_stage2(RegT
         if (q < qe) dr[fpad(q - q0)] = snv[c];
     }
     __syncthreads();
+    SG_TP(bf.tprof_az, 5);
     // per (class, section) statistics of the softmax, deterministic order
     const uint16_t *sg = tb.seg + ((size_t)t * tb.Q + m2) * (tb.Lblk + 1);
     T *pm = bf.part + (((size_t)cw * tb.nT + t) * tb.Q + m2) * 3 * (size_t)tb.Lblk;
@@ -428,9 +447,11 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_az_stage2(RegT
         pm[tb.Lblk + l] = S1;
         pm[2 * tb.Lblk + l] = S2;
     }
+    SG_TP(bf.tprof_az, 6);
     // s to HBM last (from the class-ordered LDS copy): stores count in vmcnt,
     // so they stay out of the load loops
     for (int q = q0 + tid; q < qe; q += nthr) s[q] = dr[fpad(q - q0)];
+    SG_TP(bf.tprof_az, 7);
 }
 
 // ------------------------------------------------------------------ control

@@ -45,6 +45,8 @@ struct sg_amp_plan {
     uint16_t *r_seg = nullptr;
     void *r_oc = nullptr, *r_gc = nullptr, *r_twP = nullptr, *r_twQ = nullptr, *r_stw = nullptr, *r_twa = nullptr,
          *r_twb = nullptr;
+    uint64_t *tprof = nullptr;  // diagnostics: stage-1 phase timestamps (SG_AMP_TPROF)
+    size_t tprof_items = 0;
     void *ws_s = nullptr, *ws_tu = nullptr, *ws_xn = nullptr, *ws_part = nullptr, *ws_stM = nullptr,
          *ws_stI = nullptr;
     double *ws_tau_prev = nullptr;
@@ -165,6 +167,12 @@ static int ensure_ws(sg_amp_plan *p, int B, int t_max) {
         SG_ALLOC(p->ws_tu, Bz * p->nT * p->rQ * p->nRmax * 2 * rs);
         SG_ALLOC(p->ws_xn, Bz * p->nT * p->nKmax * 2 * rs);
         SG_ALLOC(p->ws_part, Bz * p->nT * p->rQ * 3 * p->Lblk * rs);
+        if (std::getenv("SG_AMP_TPROF")) {  // diagnostics only
+            if (p->tprof) hipFree(p->tprof);
+            p->tprof_items = Bz * p->nT * p->rQ;
+            SG_ALLOC(p->tprof, p->tprof_items * 16 * sizeof(uint64_t));
+            SG_HIP(hipMemset(p->tprof, 0, p->tprof_items * 16 * sizeof(uint64_t)));
+        }
         SG_ALLOC(p->ws_stM, Bz * p->L * rs);
         SG_ALLOC(p->ws_stI, Bz * p->L * rs);
         SG_ALLOC(p->ws_tau_prev, Bz * p->Lc * 8);
@@ -456,6 +464,11 @@ static RegBufs<T> rbufs(const sg_amp_plan *p, int B, const void *y) {
     bf.y = (const T *)(y ? y : p->ws_y); bf.z = (T *)p->ws_z;
     bf.phi = p->ws_phi; bf.tau = p->ws_tau; bf.tau_prev = p->ws_tau_prev; bf.active = p->ws_active;
     bf.true_idx = nullptr; bf.map = p->ws_argmax; bf.ext_in = nullptr; bf.ext_out = nullptr;
+    bf.tprof_ab = bf.tprof_az = nullptr;
+    if (p->tprof && (size_t)B * p->nT * p->rQ <= p->tprof_items) {
+        bf.tprof_ab = p->tprof;
+        bf.tprof_az = p->tprof + p->tprof_items * 8;
+    }
     return bf;
 }
 
@@ -821,6 +834,7 @@ int sg_amp_plan_destroy(sg_amp_plan *p) {
     if (!p) return SG_OK;
     plan_free_ws(p);
     for (void *a : p->allocs) hipFree(a);
+    if (p->tprof) hipFree(p->tprof);
     delete p;
     return SG_OK;
 }
@@ -925,6 +939,29 @@ int sg_amp_encode_device(sg_amp_plan *p, const int32_t *d_idx, int B, void *d_x,
     hipStream_t s = pick_stream(stream);
     return p->precision == SG_F64 ? encode_impl<double>(p, d_idx, B, (double *)d_x, s)
                                   : encode_impl<float>(p, d_idx, B, (float *)d_x, s);
+}
+
+// Diagnostics: mean shader-clock cycles between the phase timestamps of the
+// last stage-1 launches (kernel 0 = reg_ab_stage1, 1 = reg_az_stage2), over
+// every workgroup that recorded them; needs SG_AMP_TPROF set at plan use.
+int sg_amp_stage_profile(sg_amp_plan *p, int kernel, double *mean_cycles, int *nphases) {
+    SG_CHECK_ARG(p && mean_cycles && nphases && (kernel == 0 || kernel == 1), "bad argument");
+    *nphases = 0;
+    if (!p->tprof) return SG_OK;
+    std::vector<uint64_t> h(p->tprof_items * 8);
+    SG_HIP(hipDeviceSynchronize());
+    SG_HIP(hipMemcpy(h.data(), p->tprof + (size_t)kernel * p->tprof_items * 8, h.size() * 8, hipMemcpyDeviceToHost));
+    double sum[8] = {0};
+    size_t n = 0;
+    for (size_t i = 0; i < p->tprof_items; ++i) {
+        const uint64_t *r = &h[i * 8];
+        if (!r[0] || !r[7]) continue;
+        ++n;
+        for (int k = 1; k < 8; ++k) sum[k] += (double)(r[k] - r[k - 1]);
+    }
+    for (int k = 0; k < 8; ++k) mean_cycles[k] = n ? sum[k] / n : 0.0;
+    *nphases = 8;
+    return SG_OK;
 }
 
 int sg_amp_apply_device(sg_amp_plan *p, int transpose, const void *d_in, int B, void *d_out, void *stream) {
