@@ -82,6 +82,7 @@ struct RegTables {
     int maxKb;                          // most needed indices in one row block
     const int32_t *nR;       // [nT]
     const int32_t *row_k1;   // [nT][nRmax]
+    const uint32_t *row_k1p; // [nT][EPT/2][P/EPT] rows (tid + 2j nthr, + nthr) as 16-bit pairs (stage-1 order)
     const int32_t *kptr;     // [nT][nRmax+1] needed indices of each row (CSR, within t)
     const int32_t *kk2;      // [nT][nKmax]
     const int32_t *krho;     // [nT][nKmax]

@@ -144,6 +144,13 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_ab_stage1(RegT
         const int32_t *cj = tb.cls_j + tc;
         for (int q = q0 + tid; q < q1; q += nthr) dr[ls[q] & 0xffffu] = x[cj[q]];
     }
+    // output row indices (16-bit pairs; at most P = EPT nthr rows), in flight
+    // under the FFT
+    const int nR = (tb.skip & 4) ? 0 : tb.nR[t];
+    uint32_t kp[EPT / 2];
+    const uint32_t *rkp = tb.row_k1p + (size_t)t * (tb.P / 2);
+#pragma unroll
+    for (int j = 0; j < EPT / 2; ++j) kp[j] = rkp[j * nthr + tid];
     __syncthreads();
     SG_TP(bf.tprof_ab, 2);
     if (!(tb.skip & 1)) {
@@ -151,20 +158,12 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_ab_stage1(RegT
         else lds_fft1<T, false, EPT>(d, tb.log2P, tb.stw, tid, nthr);
     }
     SG_TP(bf.tprof_ab, 3);
-    const int nR = (tb.skip & 4) ? 0 : tb.nR[t];
-    const int32_t *rk = tb.row_k1 + (size_t)t * tb.nRmax;
     cx<T> *out = bf.tu + (((size_t)cw * tb.nT + t) * tb.Q + m2) * tb.nRmax;
-    // at most P = EPT * nthr rows: every row index is loaded before any store
-    int k1[EPT];
 #pragma unroll
     for (int i = 0; i < EPT; ++i) {
         const int r = tid + i * nthr;
-        k1[i] = r < nR ? rk[r] : 0;
-    }
-#pragma unroll
-    for (int i = 0; i < EPT; ++i) {
-        const int r = tid + i * nthr;
-        if (r < nR) out[r] = cmul(d[fsw(k1[i])], cmul(ta[k1[i] & 63], tbb[k1[i] >> 6]));
+        const int k1 = (kp[i >> 1] >> (16 * (i & 1))) & 0xffff;
+        if (r < nR) out[r] = cmul(d[fsw(k1)], cmul(ta[k1 & 63], tbb[k1 >> 6]));
     }
     if (bf.tprof_ab) {
         SG_TP(bf.tprof_ab, 4); SG_TP(bf.tprof_ab, 5); SG_TP(bf.tprof_ab, 6); SG_TP(bf.tprof_ab, 7);
@@ -316,6 +315,20 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_az_stage2(RegT
     if (bf.mode == 0 && !bf.active[cw] && !tb.skip) return;
     const int tid = threadIdx.x, nthr = blockDim.x;
     SG_TP(bf.tprof_az, 0);
+    // one round trip: the U rows of this class (at most P = EPT nthr; row
+    // indices as 16-bit pairs) and the statistics of the previous beta
+    const int nR = (tb.skip & 4) ? 0 : tb.nR[t];
+    const uint32_t *rkp = tb.row_k1p + (size_t)t * (tb.P / 2);
+    const cx<T> *src = bf.tu + (((size_t)cw * tb.nT + t) * tb.Q + m2) * tb.nRmax;
+    uint32_t kp[EPT / 2];
+    cx<T> u[EPT];
+#pragma unroll
+    for (int j = 0; j < EPT / 2; ++j) kp[j] = rkp[j * nthr + tid];
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+        const int r = tid + i * nthr;
+        if (r < nR) u[i] = src[r];
+    }
     if (!(tb.skip & 16))
         for (int i = tid; i < tb.P * (int)sizeof(cx<T>) / 16; i += nthr) reinterpret_cast<uint4 *>(smem)[i] = uint4{0, 0, 0, 0};
     T tp = T(1), inv_tp = T(1);
@@ -332,24 +345,9 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_az_stage2(RegT
     }
     __syncthreads();
     SG_TP(bf.tprof_az, 1);
-    const int nR = (tb.skip & 4) ? 0 : tb.nR[t];
-    const int32_t *rk = tb.row_k1 + (size_t)t * tb.nRmax;
-    const cx<T> *src = bf.tu + (((size_t)cw * tb.nT + t) * tb.Q + m2) * tb.nRmax;
-    for (int base = tid; base < nR; base += REG_CH * nthr) {
-        int k1[REG_CH];
-        cx<T> v[REG_CH];
 #pragma unroll
-        for (int i = 0; i < REG_CH; ++i) {
-            const int r = base + i * nthr;
-            if (r < nR) {
-                k1[i] = rk[r];
-                v[i] = src[r];
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < REG_CH; ++i)
-            if (base + i * nthr < nR) d[fsw(k1[i])] = v[i];
-    }
+    for (int i = 0; i < EPT; ++i)
+        if (tid + i * nthr < nR) d[fsw((kp[i >> 1] >> (16 * (i & 1))) & 0xffff)] = u[i];
     __syncthreads();
     SG_TP(bf.tprof_az, 2);
     if (!(tb.skip & 1)) {

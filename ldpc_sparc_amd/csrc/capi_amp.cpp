@@ -38,6 +38,7 @@ struct sg_amp_plan {
     // regular engine (one transform per column block, amp_fused.hip)
     bool regular = false;
     int rP = 0, rQ = 0, rlog2P = 0, rept = 0, rmaxcls = 0, rimg = 0, nRmax = 0, nKmax = 0, RB = 0, nrb = 0, maxKb = 0, Lblk = 0, nB = 0;
+    uint32_t *r_row_k1p = nullptr;
     int32_t *r_nR = nullptr, *r_row_k1 = nullptr, *r_kptr = nullptr, *r_kk2 = nullptr, *r_krho = nullptr;
     int32_t *r_oa = nullptr, *r_ob = nullptr, *r_gi = nullptr, *r_cls_ptr = nullptr, *r_cls_j = nullptr,
             *r_qpos = nullptr;
@@ -410,6 +411,21 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
     }
     SG_TRY(upload(p, &p->r_nR, nR));
     SG_TRY(upload(p, &p->r_row_k1, f_rk));
+    {  // stage-1 order: thread tid holds rows tid + i nthr, i < ept, packed in pairs
+        const int ept = p->rept, nthr = P / ept;
+        SG_CHECK_ARG(P <= 65536 && ept % 2 == 0, "stage-1 FFT length %d exceeds the 16-bit row index", P);
+        std::vector<uint32_t> pk((size_t)nT * (P / 2), 0u);
+        for (int t = 0; t < nT; ++t) {
+            const int nr = (int)row_k1[t].size();
+            for (int j = 0; j < ept / 2; ++j)
+                for (int tid = 0; tid < nthr; ++tid) {
+                    const int r0 = tid + 2 * j * nthr, r1 = r0 + nthr;
+                    const uint32_t a = r0 < nr ? (uint32_t)row_k1[t][r0] : 0u, b = r1 < nr ? (uint32_t)row_k1[t][r1] : 0u;
+                    pk[(size_t)t * (P / 2) + (size_t)j * nthr + tid] = a | (b << 16);
+                }
+        }
+        SG_TRY(upload(p, &p->r_row_k1p, pk));
+    }
     SG_TRY(upload(p, &p->r_kptr, f_kp));
     SG_TRY(upload(p, &p->r_kk2, f_k2));
     SG_TRY(upload(p, &p->r_krho, f_kr));
@@ -442,7 +458,7 @@ static RegTables<T> rtables(const sg_amp_plan *p) {
     tb.nT = p->nT; tb.L = p->L; tb.M = p->M; tb.LM = p->LM; tb.n = p->n; tb.Lc = p->Lc; tb.Mc = p->Mc;
     tb.Lblk = p->Lblk; tb.N2 = p->N2; tb.P = p->rP; tb.Q = p->rQ; tb.log2P = p->rlog2P; tb.ept = p->rept; tb.maxcls = p->rmaxcls; tb.img = p->rimg;
     tb.nRmax = p->nRmax; tb.nKmax = p->nKmax; tb.RB = p->RB; tb.nrb = p->nrb; tb.maxKb = p->maxKb;
-    tb.nR = p->r_nR; tb.row_k1 = p->r_row_k1; tb.kptr = p->r_kptr; tb.kk2 = p->r_kk2; tb.krho = p->r_krho;
+    tb.nR = p->r_nR; tb.row_k1 = p->r_row_k1; tb.row_k1p = p->r_row_k1p; tb.kptr = p->r_kptr; tb.kk2 = p->r_kk2; tb.krho = p->r_krho;
     tb.oa = p->r_oa; tb.ob = p->r_ob; tb.oc = (const cx<T> *)p->r_oc; tb.gi = p->r_gi; tb.gc = (const cx<T> *)p->r_gc;
     tb.cls_ptr = p->r_cls_ptr; tb.cls_ls = p->r_cls_ls; tb.cls_j = p->r_cls_j;
     tb.qpos = p->r_qpos; tb.seg = p->r_seg;
