@@ -101,6 +101,7 @@ struct RegTables {
     int nB;                   // ceil(P / 64)
     int ept;                  // stage-1 FFT elements per thread (block = P / ept)
     int maxcls;               // largest class (entries of one m2 within a column block)
+    int stagger;              // first-wave start offset of odd workgroups, cycles (SG_AMP_STAGGER)
     int img;                  // reals of the stage-1 LDS image: max(2P, fpad(maxcls + 16))
     int skip;                 // timing ablation only (SG_AMP_SKIP): 1 FFT, 2 gather/scatter, 4 row I/O
 };

@@ -73,6 +73,18 @@ __device__ __forceinline__ double reg_block_sum(double v, double *red) {
         if ((buf) && tid == 0) (buf)[(((size_t)cw * tb.nT + t) * tb.Q + m2) * 8 + (k)] = __builtin_readcyclecounter(); \
     } while (0)
 
+// Workgroups of the first wave with an odd linear index start `cycles` late,
+// so that half the CUs run their memory phases while the other half computes
+// (the CUs would otherwise stay in phase and alternate between saturating HBM
+// and leaving it idle).
+__device__ __forceinline__ void reg_stagger(int cycles) {
+    if (cycles <= 0) return;
+    const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    if (lin < 256 && (lin & 1)) {
+        for (int c = 0; c < cycles; c += 8128) __builtin_amdgcn_s_sleep(127);
+    }
+}
+
 constexpr int REG_CH = 8;  // entries a thread loads before using them
 
 // block size of a stage-1 kernel: P / EPT for the compile-time sizes
@@ -97,6 +109,7 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_ab_stage1(RegT
     const int m2 = blockIdx.x, t = blockIdx.y, cw = blockIdx.z;
     if (bf.mode == 0 && !bf.active[cw] && !tb.skip) return;
     const int tid = threadIdx.x, nthr = blockDim.x;
+    reg_stagger(tb.stagger);
     SG_TP(bf.tprof_ab, 0);
     if (!(tb.skip & 16))
         for (int i = tid; i < tb.P * (int)sizeof(cx<T>) / 16; i += nthr) reinterpret_cast<uint4 *>(smem)[i] = uint4{0, 0, 0, 0};
@@ -314,6 +327,7 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_az_stage2(RegT
     const int m2 = blockIdx.x, t = blockIdx.y, cw = blockIdx.z;
     if (bf.mode == 0 && !bf.active[cw] && !tb.skip) return;
     const int tid = threadIdx.x, nthr = blockDim.x;
+    reg_stagger(tb.stagger);
     SG_TP(bf.tprof_az, 0);
     // one round trip: the U rows of this class (at most P = EPT nthr; row
     // indices as 16-bit pairs) and the statistics of the previous beta
