@@ -547,26 +547,43 @@ __global__ __launch_bounds__(1024) void reg_merge(RegTables<T> tb, RegBufs<T> bf
             if constexpr (kRestSums<T>) {
                 // partials hold (max, sums without the max); the section's
                 // designated maximum is the first partial attaining M
+                // MC partials per round trip (independent loads issued together)
+                constexpr int MC = 8;
                 T M = -INFINITY;
                 int pmx = -1;
-                for (int m2 = 0; m2 < tb.Q; ++m2) {
-                    const T mv = pm[(size_t)m2 * 3 * Lb + ll];
-                    if (mv > M) {
-                        M = mv;
-                        pmx = m2;
-                    }
+                for (int m0 = 0; m0 < tb.Q; m0 += MC) {
+                    T mv[MC];
+#pragma unroll
+                    for (int i = 0; i < MC; ++i) mv[i] = m0 + i < tb.Q ? pm[(size_t)(m0 + i) * 3 * Lb + ll] : T(-INFINITY);
+#pragma unroll
+                    for (int i = 0; i < MC; ++i)
+                        if (mv[i] > M) {
+                            M = mv[i];
+                            pmx = m0 + i;
+                        }
                 }
                 T R1 = T(0), R2 = T(0);
-                for (int m2 = 0; m2 < tb.Q; ++m2) {
-                    const T *p = pm + (size_t)m2 * 3 * Lb;
-                    if (!(p[ll] > -INFINITY)) continue;  // empty segment
-                    if (m2 == pmx) {
-                        R1 += p[Lb + ll];
-                        R2 += p[2 * Lb + ll];
-                    } else {
-                        const T f = rexp<T>(sm_arg<T>(p[ll], M, tau, inv_tau));
-                        R1 += (T(1) + p[Lb + ll]) * f;
-                        R2 += (T(1) + p[2 * Lb + ll]) * (f * f);
+                for (int m0 = 0; m0 < tb.Q; m0 += MC) {
+                    T mv[MC], s1[MC], s2[MC];
+#pragma unroll
+                    for (int i = 0; i < MC; ++i) {
+                        const T *p = pm + (size_t)(m0 + i) * 3 * Lb;
+                        const bool in = m0 + i < tb.Q;
+                        mv[i] = in ? p[ll] : T(-INFINITY);
+                        s1[i] = in ? p[Lb + ll] : T(0);
+                        s2[i] = in ? p[2 * Lb + ll] : T(0);
+                    }
+#pragma unroll
+                    for (int i = 0; i < MC; ++i) {
+                        if (!(mv[i] > -INFINITY)) continue;  // empty segment
+                        if (m0 + i == pmx) {
+                            R1 += s1[i];
+                            R2 += s2[i];
+                        } else {
+                            const T f = rexp<T>(sm_arg<T>(mv[i], M, tau, inv_tau));
+                            R1 += (T(1) + s1[i]) * f;
+                            R2 += (T(1) + s2[i]) * (f * f);
+                        }
                     }
                 }
                 const T inv = T(1) / (T(1) + R1);
