@@ -105,6 +105,24 @@ class Dist:
             self.dist.destroy_process_group()
 
 
+class HostCounterComm:
+    """Counter all-reduce through gloo on the host: only for rehearsals in which
+    several ranks share one GPU (RCCL needs one GPU per rank)."""
+
+    def __init__(self, d):
+        self.d = d
+
+    def allreduce_sum_i64(self, dbuf, count):
+        import torch
+        v = dbuf.download(np.zeros(count, np.int64))
+        t = torch.from_numpy(v)
+        self.d.dist.all_reduce(t)
+        dbuf.upload(t.numpy())
+
+    def destroy(self):
+        pass
+
+
 # ------------------------------------------------------------------ AMP (C2)
 
 def amp_setup(args, rank):
@@ -280,9 +298,13 @@ def main():
     ndev = _native.device_count()
     _native.check(_native.lib().sg_set_device(d.local % max(ndev, 1)))
     comm = None
+    counter_path = "none"
     if d.world > 1:
-        uid = d.bcast_bytes(_native.Comm.unique_id() if d.rank == 0 else None)
-        comm = _native.Comm(d.world, d.rank, uid)
+        if d.world > ndev and os.environ.get("BENCH_FORCE_RCCL") != "1":
+            comm, counter_path = HostCounterComm(d), "gloo (ranks share a GPU: rehearsal only)"
+        else:
+            uid = d.bcast_bytes(_native.Comm.unique_id() if d.rank == 0 else None)
+            comm, counter_path = _native.Comm(d.world, d.rank, uid), "rccl"
 
     st = amp_setup(args, d.rank)
     for _ in range(args.warmup):
@@ -330,7 +352,8 @@ def main():
                    "L": st["L"], "M": st["M"], "n": st["n"], "R": args.rate, "P": 15.0,
                    "awgn_var": 1.0, "t_max": args.t_max, "batch_per_gpu": st["B"],
                    "parallelism": f"mc-shard x{d.world} (independent codewords per GPU, "
-                                  "RCCL all-reduce of error counters)"},
+                                  "RCCL all-reduce of error counters)",
+                   "counter_allreduce": counter_path},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                      "traffic_unit": "HBM bytes per codeword-iteration (PMC FETCH_SIZE*2 + WRITE_SIZE, "
