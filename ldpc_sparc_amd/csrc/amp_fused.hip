@@ -426,6 +426,32 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_az_stage2(RegT
     constexpr int RC = 16;  // LDS reads in flight per thread
     for (int l = tid; l < ((tb.skip & 8) ? 0 : tb.Lblk); l += nthr) {
         const int a = sg[l], b = sg[l + 1];
+        if constexpr (kRestSums<T>) {
+            // f32: one pass with a running maximum; the sums exclude the first
+            // occurrence of the maximum and are rescaled when it moves
+            // (S <- (S + 1) e^{(m_old - m_new)/tau}), one exp per entry
+            T m = -INFINITY, S1 = T(0), S2 = T(0);
+            for (int c = a; c < b; c += RC) {
+                T v[RC];
+#pragma unroll
+                for (int i = 0; i < RC; ++i) v[i] = dr[fpad(c + i)];  // in bounds of the LDS image; masked below
+#pragma unroll
+                for (int i = 0; i < RC; ++i)
+                    if (c + i < b) {
+                        const bool up = v[i] > m;
+                        // <= 0; -inf on the first entry, whose (S + 1) e then vanishes
+                        const T dlt = up ? (m - v[i]) : (v[i] - m);
+                        const T e = rexp<T>(dlt * inv_tau);
+                        S1 = up ? (S1 + T(1)) * e : S1 + e;
+                        S2 = up ? (S2 + T(1)) * (e * e) : S2 + e * e;
+                        m = up ? v[i] : m;
+                    }
+            }
+            pm[l] = m;
+            pm[tb.Lblk + l] = S1;
+            pm[2 * tb.Lblk + l] = S2;
+            continue;
+        }
         T m = -INFINITY;
         for (int c = a; c < b; c += RC) {
             T v[RC];
