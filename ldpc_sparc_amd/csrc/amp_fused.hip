@@ -493,59 +493,114 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_az_stage2(RegT
 }
 
 // ------------------------------------------------------------------ control
-// Before Az (sparc.py:931-969): Onsager residual, phi, tau.  Lr = 1.
+// Before Az (sparc.py:931-969): Onsager residual, phi, tau.  Lr = 1.  One
+// workgroup per codeword; scalars stay in registers (no global re-reads), the
+// residual's table loads are issued a round ahead of their X gathers, and
+// |z|^2 for phi accumulates as z is written.
 template <typename T>
-__global__ __launch_bounds__(256) void reg_ctrl0(RegTables<T> tb, RegBufs<T> bf, AmpScalars sc, AmpParams pr,
-                                                 int t) {
+__global__ __launch_bounds__(1024) void reg_ctrl0(RegTables<T> tb, RegBufs<T> bf, AmpScalars sc, AmpParams pr,
+                                                  int t) {
     __shared__ double red[16];
-    __shared__ double sh_b;
-    const int cw = blockIdx.x, tid = threadIdx.x;
+    __shared__ double sh_g;
+    const int cw = blockIdx.x, tid = threadIdx.x, nthr = blockDim.x;
     if (!bf.active[cw]) return;
     const int Lc = tb.Lc;
     double *psi = sc.psi + (size_t)cw * Lc, *psi_prev = sc.psi_prev + (size_t)cw * Lc;
     double *tau = bf.tau + (size_t)cw * Lc, *tau_prev = bf.tau_prev + (size_t)cw * Lc;
     T *z = bf.z + (size_t)cw * tb.n;
     const T *y = bf.y + (size_t)cw * tb.n;
+    const bool sum_z = pr.phi_method != 1;
+    double acc = 0.0;
     if (t > 0) {
         if (tid == 0) {
-            for (int c = 0; c < Lc; ++c) {
-                psi_prev[c] = psi[c];
-                tau_prev[c] = tau[c];
-            }
-            sc.phi_prev[cw] = bf.phi[cw];
             double g = 0.0;  // ndim 0: W * psi; ndim 1: dot(W, psi) / Lc
-            for (int c = 0; c < Lc; ++c) g += pr.W[c] * psi[c];
-            sc.gamma[cw] = g / Lc;
-            sc.bcoef[cw] = sc.gamma[cw] / sc.phi_prev[cw];
-            sh_b = sc.bcoef[cw];
+            for (int c = 0; c < Lc; ++c) {
+                const double ps = psi[c];
+                psi_prev[c] = ps;
+                tau_prev[c] = tau[c];
+                g += pr.W[c] * ps;
+            }
+            const double ph = bf.phi[cw];
+            g = g / Lc;
+            sc.phi_prev[cw] = ph;
+            sc.gamma[cw] = g;
+            sc.bcoef[cw] = g / ph;
+            sh_g = g;
+            red[0] = g / ph;
         }
         __syncthreads();
-        const T b = (T)sh_b;
+        const T b = (T)red[0];
         const cx<T> *X = bf.xn + (size_t)cw * tb.nT * tb.nKmax;
-        for (int i = tid; i < tb.n; i += blockDim.x) z[i] = (y[i] - reg_ab_out(tb, X, i)) + b * z[i];
+        // reg_ab_out for CO outputs per thread at a time: every table load of
+        // the round issued before the dependent X gathers
+        constexpr int CO = 8;
+        for (int i0 = tid; i0 < tb.n; i0 += CO * nthr) {
+            T r[CO], yv[CO], zv[CO];
+#pragma unroll
+            for (int k = 0; k < CO; ++k) {
+                const int i = i0 + k * nthr;
+                r[k] = T(0);
+                if (i < tb.n) {
+                    yv[k] = y[i];
+                    zv[k] = z[i];
+                }
+            }
+            for (int t2 = 0; t2 < tb.nT; ++t2) {
+                int ia[CO], ib[CO];
+                cx<T> c1[CO], c2[CO], ha[CO], hb[CO];
+#pragma unroll
+                for (int k = 0; k < CO; ++k) {
+                    const size_t o = (size_t)t2 * tb.n + i0 + k * nthr;
+                    if (i0 + k * nthr < tb.n) {
+                        ia[k] = tb.oa[o];
+                        ib[k] = tb.ob[o];
+                        c1[k] = tb.oc[2 * o];
+                        c2[k] = tb.oc[2 * o + 1];
+                    }
+                }
+                const cx<T> *Xt = X + (size_t)t2 * tb.nKmax;
+#pragma unroll
+                for (int k = 0; k < CO; ++k)
+                    if (i0 + k * nthr < tb.n) {
+                        ha[k] = Xt[ia[k]];
+                        hb[k] = Xt[ib[k]];
+                    }
+#pragma unroll
+                for (int k = 0; k < CO; ++k)
+                    if (i0 + k * nthr < tb.n)
+                        r[k] += (c1[k].x * ha[k].x - c1[k].y * ha[k].y) + (c2[k].x * hb[k].x + c2[k].y * hb[k].y);
+            }
+#pragma unroll
+            for (int k = 0; k < CO; ++k)
+                if (i0 + k * nthr < tb.n) {
+                    const T zn = (yv[k] - r[k]) + b * zv[k];
+                    z[i0 + k * nthr] = zn;
+                    if (sum_z) acc += (double)zn * (double)zn;
+                }
+        }
     } else {
-        for (int i = tid; i < tb.n; i += blockDim.x) z[i] = y[i];
+        for (int i = tid; i < tb.n; i += nthr) {
+            const T v = y[i];
+            z[i] = v;
+            if (sum_z) acc += (double)v * (double)v;
+        }
         if (tid == 0) {
             double g = 0.0;
             for (int c = 0; c < Lc; ++c) g += pr.W[c];
-            sc.gamma[cw] = g / Lc;
+            g = g / Lc;
+            sc.gamma[cw] = g;
+            sh_g = g;
         }
     }
-    __syncthreads();
-    if (pr.phi_method == 1) {
-        if (tid == 0) bf.phi[cw] = pr.awgn_var + sc.gamma[cw];
+    double phi;
+    if (sum_z) {
+        phi = reg_block_sum(acc, red) / (double)tb.n;
     } else {
-        double acc = 0.0;
-        for (int i = tid; i < tb.n; i += blockDim.x) {
-            const double v = (double)z[i];
-            acc += v * v;
-        }
-        acc = reg_block_sum(acc, red);
-        if (tid == 0) bf.phi[cw] = acc / (double)tb.n;
+        __syncthreads();
+        phi = pr.awgn_var + sh_g;
     }
-    __syncthreads();
     if (tid == 0) {
-        const double phi = bf.phi[cw];
+        bf.phi[cw] = phi;
         for (int c = 0; c < Lc; ++c) tau[c] = (tb.L * phi / tb.n) / pr.W[c];
     }
 }
@@ -820,7 +875,7 @@ int reg_launch_ctrl0(const RegTables<T> &tb, const RegBufs<T> &bf, const AmpScal
                      hipStream_t s) {
     if (bf.B <= 0) return SG_OK;
     ProfScope ps(SG_PH_CONTROL, s);
-    hipLaunchKernelGGL((reg_ctrl0<T>), dim3(bf.B), dim3(256), 0, s, tb, bf, sc, pr, t);
+    hipLaunchKernelGGL((reg_ctrl0<T>), dim3(bf.B), dim3(1024), 0, s, tb, bf, sc, pr, t);
     SG_HIP(hipGetLastError());
     return SG_OK;
 }
