@@ -288,6 +288,11 @@ int sg_amp_encode_device(sg_amp_plan *p, const int32_t *d_idx, int B, void *d_x,
  * timestamp k minus timestamp k-1).  Only with SG_AMP_TPROF set in the
  * environment; otherwise *nphases = 0. */
 int sg_amp_stage_profile(sg_amp_plan *p, int kernel, double *mean_cycles, int *nphases);
+/* Diagnostics: the raw phase timestamps behind sg_amp_stage_profile, [items][10]:
+ * 8 shader-clock values (per-XCD clocks) then the start and end on the 100 MHz
+ * device-wide realtime clock, of the last iteration (items = B * column blocks * classes);
+ * *items = 0 when SG_AMP_TPROF was not set.  out may be null to query *items. */
+int sg_amp_stage_raw(sg_amp_plan *p, int kernel, uint64_t *out, size_t *items);
 int sg_amp_apply_device(sg_amp_plan *p, int transpose, const void *d_in, int B, void *d_out,
                         void *stream);
 /* Adds {section errors, bit errors (popcount of index XOR, MSB-first bits as

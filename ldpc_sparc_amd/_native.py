@@ -104,6 +104,7 @@ SIGNATURES = [
                                          ct.c_int, ct.c_int, ct.c_int, vp, vp]),
     ("sg_amp_encode_device", ct.c_int, [vp, vp, ct.c_int, vp, vp]),
     ("sg_amp_stage_profile", ct.c_int, [vp, ct.c_int, vp, vp]),
+    ("sg_amp_stage_raw", ct.c_int, [vp, ct.c_int, vp, vp]),
     # device encoder and channel
     ("sg_rng_bits_device", ct.c_int, [ct.c_uint64, ct.c_uint64, ct.c_int, ct.c_int, vp, vp]),
     ("sg_bits_to_sections_device", ct.c_int, [vp, ct.c_int, ct.c_int, ct.c_int, vp, vp]),

@@ -124,6 +124,7 @@ struct RegBufs {
     const T *ext_in;        // mode 1: [B][LM] (Ab) or [B][n] (Az)
     T *ext_out;             // mode 1: [B][n] (Ab) or [B][LM] (Az)
     uint64_t *tprof_ab, *tprof_az;  // diagnostics (SG_AMP_TPROF): [B][nT][Q][8] phase timestamps, or null
+    uint64_t *trt_ab, *trt_az;      // diagnostics: [B][nT][Q][2] realtime start / end
 };
 
 template <typename T>

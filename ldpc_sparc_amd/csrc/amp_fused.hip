@@ -68,9 +68,15 @@ __device__ __forceinline__ double reg_block_sum(double v, double *red) {
 }
 
 // diagnostics: wave 0 of a workgroup stamps the shader clock at phase k
+// (and, at the first and last phase, the device-wide 100 MHz realtime clock)
 #define SG_TP(buf, k)                                                                                           \
     do {                                                                                                        \
-        if ((buf) && tid == 0) (buf)[(((size_t)cw * tb.nT + t) * tb.Q + m2) * 8 + (k)] = __builtin_readcyclecounter(); \
+        if ((buf) && tid == 0) {                                                                                \
+            const size_t it_ = ((size_t)cw * tb.nT + t) * tb.Q + m2;                                             \
+            (buf)[it_ * 8 + (k)] = __builtin_readcyclecounter();                                                \
+            if ((k) == 0 || (k) == 7)                                                                           \
+                ((buf) == bf.tprof_ab ? bf.trt_ab : bf.trt_az)[it_ * 2 + ((k) == 7)] = __builtin_amdgcn_s_memrealtime(); \
+        }                                                                                                       \
     } while (0)
 
 // Workgroups of the first wave with an odd linear index start `cycles` late,
@@ -179,7 +185,9 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_ab_stage1(RegT
         if (r < nR) out[r] = cmul(d[fsw(k1)], cmul(ta[k1 & 63], tbb[k1 >> 6]));
     }
     if (bf.tprof_ab) {
-        SG_TP(bf.tprof_ab, 4); SG_TP(bf.tprof_ab, 5); SG_TP(bf.tprof_ab, 6); SG_TP(bf.tprof_ab, 7);
+        SG_TP(bf.tprof_ab, 4); SG_TP(bf.tprof_ab, 5); SG_TP(bf.tprof_ab, 6);
+        __syncthreads();  // diagnostics only: the end stamp waits for every wavefront
+        SG_TP(bf.tprof_ab, 7);
     }
 }
 
@@ -489,6 +497,7 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_az_stage2(RegT
     // s to HBM last (from the class-ordered LDS copy): stores count in vmcnt,
     // so they stay out of the load loops
     for (int q = q0 + tid; q < qe; q += nthr) s[q] = dr[fpad(q - q0)];
+    if (bf.tprof_az) __syncthreads();  // diagnostics only: the end stamp waits for every wavefront
     SG_TP(bf.tprof_az, 7);
 }
 

@@ -171,8 +171,9 @@ static int ensure_ws(sg_amp_plan *p, int B, int t_max) {
         if (std::getenv("SG_AMP_TPROF")) {  // diagnostics only
             if (p->tprof) hipFree(p->tprof);
             p->tprof_items = Bz * p->nT * p->rQ;
-            SG_ALLOC(p->tprof, p->tprof_items * 16 * sizeof(uint64_t));
-            SG_HIP(hipMemset(p->tprof, 0, p->tprof_items * 16 * sizeof(uint64_t)));
+            // [2 kernels][items][8] shader-clock stamps, then [2 kernels][items][2] realtime start / end
+            SG_ALLOC(p->tprof, p->tprof_items * 20 * sizeof(uint64_t));
+            SG_HIP(hipMemset(p->tprof, 0, p->tprof_items * 20 * sizeof(uint64_t)));
         }
         SG_ALLOC(p->ws_stM, Bz * p->L * rs);
         SG_ALLOC(p->ws_stI, Bz * p->L * rs);
@@ -484,10 +485,12 @@ static RegBufs<T> rbufs(const sg_amp_plan *p, int B, const void *y) {
     bf.y = (const T *)(y ? y : p->ws_y); bf.z = (T *)p->ws_z;
     bf.phi = p->ws_phi; bf.tau = p->ws_tau; bf.tau_prev = p->ws_tau_prev; bf.active = p->ws_active;
     bf.true_idx = nullptr; bf.map = p->ws_argmax; bf.ext_in = nullptr; bf.ext_out = nullptr;
-    bf.tprof_ab = bf.tprof_az = nullptr;
+    bf.tprof_ab = bf.tprof_az = bf.trt_ab = bf.trt_az = nullptr;
     if (p->tprof && (size_t)B * p->nT * p->rQ <= p->tprof_items) {
         bf.tprof_ab = p->tprof;
         bf.tprof_az = p->tprof + p->tprof_items * 8;
+        bf.trt_ab = p->tprof + p->tprof_items * 16;
+        bf.trt_az = p->tprof + p->tprof_items * 18;
     }
     return bf;
 }
@@ -981,6 +984,24 @@ int sg_amp_stage_profile(sg_amp_plan *p, int kernel, double *mean_cycles, int *n
     }
     for (int k = 0; k < 8; ++k) mean_cycles[k] = n ? sum[k] / n : 0.0;
     *nphases = 8;
+    return SG_OK;
+}
+
+int sg_amp_stage_raw(sg_amp_plan *p, int kernel, uint64_t *out, size_t *items) {
+    SG_CHECK_ARG(p && items && (kernel == 0 || kernel == 1), "bad argument");
+    *items = p->tprof ? p->tprof_items : 0;
+    if (!p->tprof || !out) return SG_OK;
+    const size_t ni = p->tprof_items;
+    std::vector<uint64_t> cyc(ni * 8), rt(ni * 2);
+    SG_HIP(hipDeviceSynchronize());
+    SG_HIP(hipMemcpy(cyc.data(), p->tprof + (size_t)kernel * ni * 8, ni * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    SG_HIP(hipMemcpy(rt.data(), p->tprof + ni * 16 + (size_t)kernel * ni * 2, ni * 2 * sizeof(uint64_t),
+                     hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < ni; ++i) {
+        std::copy(&cyc[i * 8], &cyc[i * 8] + 8, out + i * 10);
+        out[i * 10 + 8] = rt[i * 2];
+        out[i * 10 + 9] = rt[i * 2 + 1];
+    }
     return SG_OK;
 }
 

@@ -44,3 +44,21 @@ for k, kn in ((0, "ab_stage1"), (1, "az_stage2")):
     for nm, c in zip(names[k], v):
         if nm != "-":
             print("   %-16s %8.0f cycles  %5.1f %%" % (nm, c, 100 * c / tot))
+
+# occupancy: sum of workgroup durations over the span of the launch (both in
+# shader-clock cycles); 256 = every CU busy with one workgroup all the time
+items = ct.c_size_t()
+for k, kn in ((0, "ab_stage1"), (1, "az_stage2")):
+    _native.check(lib.sg_amp_stage_raw(plan, k, None, ct.byref(items)))
+    raw = np.zeros((items.value, 10), np.uint64)
+    _native.check(lib.sg_amp_stage_raw(plan, k, raw.ctypes.data, ct.byref(items)))
+    ok = (raw[:, 8] > 0) & (raw[:, 9] > 0)
+    r = raw[ok].astype(np.float64)
+    st, en = r[:, 8] * 10.0, r[:, 9] * 10.0  # ns (100 MHz realtime clock)
+    span = en.max() - st.min()
+    dur = en - st
+    cyc = r[:, 7] - r[:, 0]
+    print("%s: %d workgroups, span %.1f us, duration mean %.2f us, p10/p50/p90 %.2f/%.2f/%.2f us, "
+          "concurrency %.1f, shader clock %.2f GHz"
+          % (kn, len(r), span / 1e3, dur.mean() / 1e3, *(np.percentile(dur, [10, 50, 90]) / 1e3),
+             dur.sum() / span, cyc.sum() / dur.sum()))
