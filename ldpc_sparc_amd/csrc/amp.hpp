@@ -28,7 +28,28 @@ struct AmpTables {
     const int32_t *gs_i;              // [4] per slot: contributing row index or -1
     const cx<T> *gs_c;                // [4] per slot: coefficient
     const cx<T> *twP, *twQ, *twHi, *twLo;
+    const int32_t *row_ptr, *row_t;   // CSR: transforms of each row block, row-major order
 };
+
+// Block engine (amp_block.hip): single precision, N2 = 2^14, one workgroup per
+// (column block, codeword) running that column's transforms in LDS.
+struct BlkTables {
+    int nT, L, M, LM, n, Lr, Lc, Mr, Mc;
+    const int32_t *col_ptr, *col_t, *t_row;
+    const uint32_t *pos2;     // [nT][8][1024] real LDS index (2 fsw(m) + component) of column entry
+                              // j = tid + 1024 i, pairs (i = 2 i2, 2 i2 + 1) at [t][i2][tid]
+    const uint32_t *oab;      // [nT][Mr] fsw(a) | fsw(b) << 16 of output i
+    const cx<float> *oc;      // [nT][Mr][2] X_i = Re(c1 H[a] + c2 conj H[b])
+    int ngs;                  // G slots of all transforms (= gptr[nT])
+    const int32_t *gptr;      // [nT + 1] G slots of each transform (CSR)
+    const int32_t *grow;      // row block of each slot's transform
+    const uint16_t *gloc;     // fsw(k) of the slot
+    const int32_t *gi;        // [4] per slot: contributing output row index (local to the row block) or -1
+    const cx<float> *gc;      // [4] per slot: coefficient
+    const cx<float> *stw;     // per-stage twiddles of the N2-point FFT (fft.hpp lds_fft1_ct, EPT 16)
+    int skip;                 // timing ablation only (SG_AMP_SKIP): 1 sections, 2 inverse FFT
+};
+size_t blk_lds_bytes(int Mc);
 
 // Per-batch device buffers.
 template <typename T>
@@ -167,6 +188,9 @@ template <typename T>
 int amp_launch_cast(const void *in, int in_is_double, T *out, size_t n, hipStream_t s);
 template <typename T>
 int amp_launch_uncast(const T *in, double *out, size_t n, hipStream_t s);
+int blk_launch_ab(const BlkTables &tb, const AmpBufs<float> &bf, hipStream_t s);   // beta -> rbuf
+int blk_launch_az(const BlkTables &tb, const AmpBufs<float> &bf, cx<float> *gbuf,
+                  hipStream_t s);  // z/phi -> G slots (gbuf [B][ngs]) -> beta, section statistics
 int amp_launch_count(const int32_t *map_idx, const int32_t *true_idx, const int32_t *t_final, int B, int L,
                      int logM, int64_t *counts, hipStream_t s);
 

@@ -1,0 +1,331 @@
+// Block engine: AMP for sub-sampled DCT designs whose transforms fit one
+// workgroup's LDS (single precision, w = 2^15, N2 = 2^14 complex points) and
+// whose base matrix has several transforms per column block -- the spatially
+// coupled designs of sparc_demo_sc_decode_wave (sparc.py:535-568 sc_basic,
+// :851-875 the per-block operators).
+//
+// Reference: sparc_public/sparc.py sparc_amp :883-999, sub_dct :648-701,
+// msg_vector_mmse_estimator :402-465, msg_vector_map_estimator :467-512.
+//
+// One workgroup owns one column block c of one codeword and runs the omega
+// transforms of that column back to back, each entirely in LDS (Makhoul-packed
+// N2-point FFT, natural order at fsw positions):
+//   blk_ab   beta_c (registers, loaded once) -> for each transform (r, c):
+//            scatter by order1, forward FFT, the Mr needed outputs
+//            Re(c1 H[a] + c2 conj H[b]) -> rbuf[t] (summed per row block in a
+//            fixed order by the control kernel)
+//   blk_az   for each transform (r, c): G from z_r / phi_r (<= 4 terms per
+//            slot), inverse FFT, gather by order1 into u (registers); then the
+//            column's sections: s = beta + tau_c u, softmax, MAP index and the
+//            section statistics of eta_kernel (amp_dct.hip), beta written back.
+// Versus the general four-step path (amp_dct.hip) no transform intermediate
+// reaches HBM and the random-order gather of u happens in LDS.
+#include "amp.hpp"
+
+namespace sg {
+
+constexpr int BK_THREADS = 1024;
+constexpr int BK_LOG2N = 14;
+constexpr int BK_J = 16;  // column entries per thread (Mc = 16384)
+
+template <typename T>
+__device__ __forceinline__ T bk_wave_max(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ T bk_wave_sum(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ int bk_wave_min(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// LDS: the FFT image, then the staged positions of one transform (blk_az);
+// the per-wave partials of the section reductions overlay the image
+size_t blk_lds_bytes(int Mc) {
+    return (size_t)(1 << BK_LOG2N) * sizeof(cx<float>) + (size_t)(BK_J / 2) * BK_THREADS * sizeof(uint32_t);
+}
+
+__device__ __forceinline__ void bk_clear(unsigned char *smem, int tid) {
+#pragma unroll
+    for (int i = 0; i < (1 << BK_LOG2N) * (int)sizeof(cx<float>) / 16 / BK_THREADS; ++i)
+        reinterpret_cast<uint4 *>(smem)[tid + i * BK_THREADS] = uint4{0, 0, 0, 0};
+}
+
+// The thread index as a value the compiler cannot see through: the FFT's LDS
+// addresses are then recomputed inside the loop over a column's transforms
+// instead of being hoisted out of it and held (and spilled) across the loop.
+__device__ __forceinline__ int bk_opaque(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+// Column entry i (< 16) of thread tid: wavefront w owns sections
+// w spw .. w spw + spw - 1 of the column block (spw = 1024 / M), lane l holds
+// entries l eps .. l eps + eps - 1 of each (eps = M / 64).  Needs Mc = 16384
+// and 64 <= M <= 1024 (host mirror in capi_amp.cpp build_block).
+template <int EPS>
+__device__ __forceinline__ int bk_j(int tid, int i) {
+    constexpr int M = 64 * EPS, SPW = 1024 / M;
+    const int sq = i / EPS, e = i - sq * EPS;
+    return ((tid >> 6) * SPW + sq) * M + (tid & 63) * EPS + e;
+}
+
+// LDS positions of the thread's column entries bk_j(tid, i) of transform t,
+// packed in pairs (i = 2 i2, 2 i2 + 1) in thread order
+__device__ __forceinline__ void bk_pos_load(const BlkTables &tb, int t, int tid, uint32_t *pv) {
+    const uint32_t *p2 = tb.pos2 + (size_t)t * (BK_J / 2) * BK_THREADS;
+#pragma unroll
+    for (int i = 0; i < BK_J / 2; ++i) pv[i] = p2[i * BK_THREADS + tid];
+}
+__device__ __forceinline__ uint32_t bk_pos(const uint32_t *pv, int i) { return (pv[i >> 1] >> (16 * (i & 1))) & 0xffffu; }
+
+// ------------------------------------------------------------------ Ab
+template <int EPS>
+__global__ __launch_bounds__(BK_THREADS) void blk_ab(BlkTables tb, AmpBufs<float> bf) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cx<float> *d = reinterpret_cast<cx<float> *>(smem);
+    float *dr = reinterpret_cast<float *>(smem);
+    const int c = blockIdx.x, cw = blockIdx.y, tid = threadIdx.x;
+    if (!bf.active[cw]) return;
+    const float *beta = bf.beta + (size_t)cw * tb.LM + (size_t)c * tb.Mc;
+    for (int q = tb.col_ptr[c]; q < tb.col_ptr[c + 1]; ++q) {
+        const int t = tb.col_t[q];
+        const int tl = bk_opaque(tid);
+        // beta_c and the positions of this transform, in flight while the image
+        // clears (beta is re-read from L2 for each transform: holding it in
+        // registers across the FFT would spill)
+        float bv[BK_J];
+#pragma unroll
+        for (int i = 0; i < BK_J; ++i) bv[i] = beta[bk_j<EPS>(tl, i)];
+        uint32_t pv[BK_J / 2];
+        bk_pos_load(tb, t, tl, pv);
+        bk_clear(smem, tl);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < BK_J; ++i)
+            dr[bk_pos(pv, i)] = bv[i];
+        __syncthreads();
+        lds_fft1_ct<float, false, 16, BK_LOG2N>(d, tb.stw, tl);
+        float *r = bf.rbuf + ((size_t)cw * tb.nT + t) * tb.Mr;
+        const uint32_t *oab = tb.oab + (size_t)t * tb.Mr;
+        const cx<float> *oc = tb.oc + (size_t)t * tb.Mr * 2;
+        for (int i = tl; i < tb.Mr; i += BK_THREADS) {
+            const uint32_t ab = oab[i];
+            const cx<float> ha = d[ab & 0xffffu], hb = d[ab >> 16];
+            const cx<float> c1 = oc[2 * i], c2 = oc[2 * i + 1];
+            r[i] = (c1.x * ha.x - c1.y * ha.y) + (c2.x * hb.x + c2.y * hb.y);  // Re(c1 ha + c2 conj hb)
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------ G slots
+// Packed spectrum of Az's input for every transform (sparc.py:694-699 via the
+// Makhoul packing): G[k] = sum of <= 4 terms c * z_i / phi_r, one thread per
+// slot, written to gbuf so that blk_az loads each transform's slots in one
+// coalesced round trip.
+__global__ __launch_bounds__(256) void blk_g(BlkTables tb, AmpBufs<float> bf, cx<float> *gbuf) {
+    const int cw = blockIdx.y;
+    if (!bf.active[cw]) return;
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= tb.ngs) return;
+    const int row = tb.grow[g];
+    const float *z = bf.z + (size_t)cw * tb.n + (size_t)row * tb.Mr;
+    const float phi = (float)bf.phi[(size_t)cw * tb.Lr + row];
+    cx<float> acc{0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int i = tb.gi[4 * g + k];
+        if (i >= 0) {
+            const float v = z[i] / phi;  // Az(z / phi), sparc.py:972
+            const cx<float> cc = tb.gc[4 * g + k];
+            acc.x += cc.x * v;
+            acc.y += cc.y * v;
+        }
+    }
+    gbuf[(size_t)cw * tb.ngs + g] = acc;
+}
+
+// ------------------------------------------------------------------ Az + eta
+template <int EPS>
+__global__ __launch_bounds__(BK_THREADS) void blk_az(BlkTables tb, AmpBufs<float> bf, const cx<float> *gbuf) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cx<float> *d = reinterpret_cast<cx<float> *>(smem);
+    float *dr = reinterpret_cast<float *>(smem);
+    // positions of the current transform's column entries, staged in LDS
+    // beside the image (held in registers across the FFT they would spill)
+    uint32_t *pl = reinterpret_cast<uint32_t *>(smem + (size_t)(1 << BK_LOG2N) * sizeof(cx<float>));
+    const int c = blockIdx.x, cw = blockIdx.y, tid = threadIdx.x;
+    if (!bf.active[cw]) return;
+    float u[BK_J];
+#pragma unroll
+    for (int i = 0; i < BK_J; ++i) u[i] = 0.f;
+    const cx<float> *gcw = gbuf + (size_t)cw * tb.ngs;
+    // Az(z / phi) restricted to column block c, summed over its transforms in
+    // the order of gather_u (amp_dct.hip)
+    for (int q = tb.col_ptr[c]; q < tb.col_ptr[c + 1]; ++q) {
+        const int t = tb.col_t[q];
+        const int tl = bk_opaque(tid);
+        // one round trip: positions and G slots, in flight while the image clears
+        uint32_t pv[BK_J / 2];
+        bk_pos_load(tb, t, tl, pv);
+        const int g0 = tb.gptr[t], ng = tb.gptr[t + 1] - g0;
+        cx<float> gv[2];
+        uint32_t gl[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int g = tl + k * BK_THREADS;
+            if (g < ng) {
+                gv[k] = gcw[g0 + g];
+                gl[k] = tb.gloc[g0 + g];
+            }
+        }
+        bk_clear(smem, tl);
+#pragma unroll
+        for (int i = 0; i < BK_J / 2; ++i) pl[i * BK_THREADS + tl] = pv[i];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            if (tl + k * BK_THREADS < ng) d[gl[k]] = gv[k];
+        for (int g = tl + 2 * BK_THREADS; g < ng; g += BK_THREADS) d[tb.gloc[g0 + g]] = gcw[g0 + g];
+        __syncthreads();
+        if (!(tb.skip & 2)) lds_fft1_ct<float, true, 16, BK_LOG2N>(d, tb.stw, tl);
+#pragma unroll
+        for (int i = 0; i < BK_J; ++i)
+            u[i] += dr[(pl[(i >> 1) * BK_THREADS + tl] >> (16 * (i & 1))) & 0xffffu];
+        __syncthreads();
+    }
+    if (tb.skip & 1) return;  // timing ablation only
+    // ---- sections of the column block (sparc.py:972, :429-432, :485-487):
+    // s = beta + tau u, x = s / tau, beta = exp(x - max) / sum, MAP = first
+    // index of max s.  A wavefront owns whole sections (bk_j): each lane
+    // reduces its EPS entries, then one butterfly over the lanes -- no LDS, no
+    // workgroup barrier.
+    const int lane = tid & 63, wv = tid >> 6;
+    constexpr int eps = EPS, spw = 1024 / (64 * EPS);
+    const int nsec = tb.Mc / tb.M;
+    const float tau = (float)bf.tau[(size_t)cw * tb.Lc + c];
+    float *beta = bf.beta + (size_t)cw * tb.LM + (size_t)c * tb.Mc;
+    float s[BK_J], x[BK_J];
+#pragma unroll
+    for (int i = 0; i < BK_J; ++i) {
+        const int j = bk_j<EPS>(tid, i);
+        s[i] = beta[j] + tau * u[i];  // sparc.py:972
+        x[i] = s[i] / tau;            // sparc.py:430
+    }
+    const int l0 = c * nsec;  // first section of the column block
+#pragma unroll
+    for (int sq = 0; sq < spw; ++sq) {
+        const int ls = wv * spw + sq;  // section within the column block
+        const int i0 = sq * eps;
+        // maxima and the MAP index (entries of a lane are in increasing j)
+        float xm = -INFINITY, sm = -INFINITY;
+        int arg = 0x7fffffff;
+#pragma unroll
+        for (int e = 0; e < eps; ++e) {
+            xm = fmax(xm, x[i0 + e]);
+            if (s[i0 + e] > sm) {
+                sm = s[i0 + e];
+                arg = lane * eps + e;
+            }
+        }
+        xm = bk_wave_max(xm);
+        const float gm = bk_wave_max(sm);
+        arg = bk_wave_min(sm == gm ? arg : 0x7fffffff);
+        float dn = 0.f;
+#pragma unroll
+        for (int e = 0; e < eps; ++e) {
+            x[i0 + e] = __expf(x[i0 + e] - xm);
+            dn += x[i0 + e];
+        }
+        dn = bk_wave_sum(dn);
+        const int truth = bf.true_idx ? bf.true_idx[(size_t)cw * tb.L + l0 + ls] : -1;
+        float ss = 0.f, se = 0.f;
+#pragma unroll
+        for (int e = 0; e < eps; ++e) {
+            const float b = x[i0 + e] / dn;
+            beta[ls * tb.M + lane * eps + e] = b;
+            const float dl = b - ((lane * eps + e) == truth ? 1.f : 0.f);
+            ss += b * b;
+            se += dl * dl;
+        }
+        ss = bk_wave_sum(ss);
+        se = bk_wave_sum(se);
+        if (lane == 0) {
+            const size_t o = (size_t)cw * tb.L + l0 + ls;
+            bf.sec_sumsq[o] = (double)ss;
+            bf.sec_err[o] = (double)se;
+            bf.sec_argmax[o] = arg;
+        }
+    }
+}
+
+template <int EPS>
+static int blk_set_attrs(size_t lds) {
+    static size_t done = 0;
+    if (done >= lds) return SG_OK;
+    SG_HIP(hipFuncSetAttribute((const void *)blk_ab<EPS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    SG_HIP(hipFuncSetAttribute((const void *)blk_az<EPS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    done = lds;
+    return SG_OK;
+}
+
+// section size M = 64 EPS, 64 <= M <= 1024 (compile-time, so the per-lane
+// entry arrays stay in registers)
+#define BK_EPS_DISPATCH(M, F, ...)                                                   \
+    switch (M) {                                                                     \
+    case 64: F<1>(__VA_ARGS__); break;                                               \
+    case 128: F<2>(__VA_ARGS__); break;                                              \
+    case 256: F<4>(__VA_ARGS__); break;                                              \
+    case 512: F<8>(__VA_ARGS__); break;                                              \
+    case 1024: F<16>(__VA_ARGS__); break;                                            \
+    default: return fail(SG_ERR_UNSUPPORTED, "block engine: section size M=%d", M); \
+    }
+
+template <int EPS>
+static void bk_launch_ab(const BlkTables &tb, const AmpBufs<float> &bf, size_t lds, hipStream_t s, int *rc) {
+    *rc = blk_set_attrs<EPS>(lds);
+    if (*rc == SG_OK) hipLaunchKernelGGL(blk_ab<EPS>, dim3(tb.Lc, bf.B), dim3(BK_THREADS), lds, s, tb, bf);
+}
+template <int EPS>
+static void bk_launch_az(const BlkTables &tb, const AmpBufs<float> &bf, const cx<float> *gbuf, size_t lds,
+                         hipStream_t s, int *rc) {
+    *rc = blk_set_attrs<EPS>(lds);
+    if (*rc == SG_OK) hipLaunchKernelGGL(blk_az<EPS>, dim3(tb.Lc, bf.B), dim3(BK_THREADS), lds, s, tb, bf, gbuf);
+}
+
+int blk_launch_ab(const BlkTables &tb, const AmpBufs<float> &bf, hipStream_t s) {
+    if (bf.B <= 0) return SG_OK;
+    const size_t lds = blk_lds_bytes(tb.Mc);
+    int rc = SG_OK;
+    ProfScope ps(SG_PH_AB_A, s);
+    BK_EPS_DISPATCH(tb.M, bk_launch_ab, tb, bf, lds, s, &rc);
+    SG_TRY(rc);
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
+int blk_launch_az(const BlkTables &tb, const AmpBufs<float> &bf, cx<float> *gbuf, hipStream_t s) {
+    if (bf.B <= 0) return SG_OK;
+    const size_t lds = blk_lds_bytes(tb.Mc);
+    {
+        ProfScope ps(SG_PH_AZ_A, s);
+        hipLaunchKernelGGL(blk_g, dim3((tb.ngs + 255) / 256, bf.B), dim3(256), 0, s, tb, bf, gbuf);
+    }
+    SG_HIP(hipGetLastError());
+    int rc = SG_OK;
+    ProfScope ps(SG_PH_AZ_B, s);
+    BK_EPS_DISPATCH(tb.M, bk_launch_az, tb, bf, (const cx<float> *)gbuf, lds, s, &rc);
+    SG_TRY(rc);
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
+}  // namespace sg

@@ -265,9 +265,9 @@ __device__ __forceinline__ double block_sum(double v, double *red) {
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void control_kernel(AmpTables<T> tb, AmpBufs<T> bf, AmpScalars sc, AmpParams pr,
-                                                      int phase, int t) {
-    __shared__ double red[8];
+__global__ __launch_bounds__(1024) void control_kernel(AmpTables<T> tb, AmpBufs<T> bf, AmpScalars sc, AmpParams pr,
+                                                       int phase, int t) {
+    __shared__ double red[16];
     const int cw = blockIdx.x, tid = threadIdx.x;
     const int Lr = tb.Lr, Lc = tb.Lc;
     double *psi = sc.psi + (size_t)cw * Lc, *psi_prev = sc.psi_prev + (size_t)cw * Lc;
@@ -286,25 +286,27 @@ __global__ __launch_bounds__(256) void control_kernel(AmpTables<T> tb, AmpBufs<T
         const T *y = bf.y + (size_t)cw * tb.n;
         if (t > 0) {
             __syncthreads();
-            if (tid == 0) {
-                for (int c = 0; c < Lc; ++c) psi_prev[c] = psi[c];
-                for (int r = 0; r < Lr; ++r) phi_prev[r] = phi[r];
-                if (tb.ndim == 0) gamma[0] = pr.W[0] * psi[0];
-                else
-                    for (int r = 0; r < Lr; ++r) {
-                        double acc = 0.0;
-                        for (int c = 0; c < Lc; ++c) acc += pr.W[r * Lc + c] * psi[c];
-                        gamma[r] = acc / Lc;
-                    }
-                for (int r = 0; r < Lr; ++r) bco[r] = gamma[r] / phi_prev[r];
+            // per row block in parallel (same per-entry arithmetic as the serial form)
+            for (int r = tid; r < Lr; r += blockDim.x) {
+                phi_prev[r] = phi[r];
+                double g;
+                if (tb.ndim == 0) g = pr.W[0] * psi[0];
+                else {
+                    double acc = 0.0;
+                    for (int c = 0; c < Lc; ++c) acc += pr.W[r * Lc + c] * psi[c];
+                    g = acc / Lc;
+                }
+                gamma[r] = g;
+                bco[r] = g / phi[r];
             }
             __syncthreads();
+            for (int c = tid; c < Lc; c += blockDim.x) psi_prev[c] = psi[c];
             // z = y - Ab(beta) + b*z, Ab summed over the transforms of each row block
             for (int i = tid; i < tb.n; i += blockDim.x) {
                 const int r = i / tb.Mr, il = i - r * tb.Mr;
                 T ab = T(0);
-                for (int q = 0; q < tb.nT; ++q)
-                    if (tb.t_row[q] == r) ab += bf.rbuf[((size_t)cw * tb.nT + q) * tb.Mr + il];
+                for (int q = tb.row_ptr[r]; q < tb.row_ptr[r + 1]; ++q)
+                    ab += bf.rbuf[((size_t)cw * tb.nT + tb.row_t[q]) * tb.Mr + il];
                 z[i] = (y[i] - ab) + (T)bco[r] * z[i];
             }
         } else {
@@ -323,43 +325,61 @@ __global__ __launch_bounds__(256) void control_kernel(AmpTables<T> tb, AmpBufs<T
         if (pr.phi_method == 1) {
             if (tid == 0)
                 for (int r = 0; r < Lr; ++r) phi[r] = pr.awgn_var + gamma[r];
-        } else {
-            for (int r = 0; r < Lr; ++r) {
-                const int i0 = (tb.ndim == 2) ? r * tb.Mr : 0, i1 = (tb.ndim == 2) ? (r + 1) * tb.Mr : tb.n;
+        } else if (tb.ndim == 2) {  // one wavefront per row block, no workgroup barriers
+            const int lane = tid & 63, nw = blockDim.x >> 6;
+            for (int r = tid >> 6; r < Lr; r += nw) {
                 double acc = 0.0;
-                for (int i = i0 + tid; i < i1; i += blockDim.x) { const double v = (double)z[i]; acc += v * v; }
-                acc = block_sum(acc, red);
-                if (tid == 0) phi[r] = acc / (double)(i1 - i0);
+                for (int i = r * tb.Mr + lane; i < (r + 1) * tb.Mr; i += 64) { const double v = (double)z[i]; acc += v * v; }
+                acc = wave_sum(acc);
+                if (lane == 0) phi[r] = acc / (double)tb.Mr;
             }
+        } else {
+            double acc = 0.0;
+            for (int i = tid; i < tb.n; i += blockDim.x) { const double v = (double)z[i]; acc += v * v; }
+            acc = block_sum(acc, red);
+            if (tid == 0) phi[0] = acc / (double)tb.n;
         }
         __syncthreads();
-        if (tid == 0) {
+        for (int c = tid; c < (tb.ndim == 0 ? 1 : Lc); c += blockDim.x) {  // per column block in parallel
             if (tb.ndim == 0) tau[0] = (tb.L * phi[0] / tb.n) / pr.W[0];
-            else if (tb.ndim == 1)
-                for (int c = 0; c < Lc; ++c) tau[c] = (tb.L * phi[0] / tb.n) / pr.W[c];
-            else
-                for (int c = 0; c < Lc; ++c) {
-                    double acc = 0.0;
-                    for (int r = 0; r < Lr; ++r) acc += pr.W[r * Lc + c] * (1.0 / phi[r]);
-                    tau[c] = ((double)tb.L / tb.Mr) / acc;
-                }
+            else if (tb.ndim == 1) tau[c] = (tb.L * phi[0] / tb.n) / pr.W[c];
+            else {
+                double acc = 0.0;
+                for (int r = 0; r < Lr; ++r) acc += pr.W[r * Lc + c] * (1.0 / phi[r]);
+                tau[c] = ((double)tb.L / tb.Mr) / acc;
+            }
         }
         return;
     }
     // phase 1: psi / NMSE / stop
     const int spc = tb.L / Lc;
-    for (int c = 0; c < Lc; ++c) {
+    const double denom = (tb.ndim == 0) ? (double)tb.L : ((double)tb.L / Lc);
+    if (Lc > 1) {  // one wavefront per column block, no workgroup barriers
+        const int lane = tid & 63, nw = blockDim.x >> 6;
+        for (int c = tid >> 6; c < Lc; c += nw) {
+            double a = 0.0, e = 0.0;
+            for (int l = c * spc + lane; l < (c + 1) * spc; l += 64) {
+                a += bf.sec_sumsq[(size_t)cw * tb.L + l];
+                e += bf.sec_err[(size_t)cw * tb.L + l];
+            }
+            a = wave_sum(a);
+            e = wave_sum(e);
+            if (lane == 0) {
+                psi[c] = 1.0 - a / denom;
+                nmse[(size_t)(t + 1) * Lc + c] = e / denom;
+            }
+        }
+    } else {
         double a = 0.0, e = 0.0;
-        for (int l = c * spc + tid; l < (c + 1) * spc; l += blockDim.x) {
+        for (int l = tid; l < spc; l += blockDim.x) {
             a += bf.sec_sumsq[(size_t)cw * tb.L + l];
             e += bf.sec_err[(size_t)cw * tb.L + l];
         }
         a = block_sum(a, red);
         e = block_sum(e, red);
         if (tid == 0) {
-            const double denom = (tb.ndim == 0) ? (double)tb.L : ((double)tb.L / Lc);
-            psi[c] = 1.0 - a / denom;
-            nmse[(size_t)(t + 1) * Lc + c] = e / denom;
+            psi[0] = 1.0 - a / denom;
+            nmse[(size_t)(t + 1) * Lc] = e / denom;
         }
     }
     __syncthreads();
@@ -389,8 +409,8 @@ __global__ void rowsum_kernel(AmpTables<T> tb, AmpBufs<T> bf, T *out) {
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < tb.n; i += gridDim.x * blockDim.x) {
         const int r = i / tb.Mr, il = i - r * tb.Mr;
         T acc = T(0);
-        for (int q = 0; q < tb.nT; ++q)
-            if (tb.t_row[q] == r) acc += bf.rbuf[((size_t)cw * tb.nT + q) * tb.Mr + il];
+        for (int q = tb.row_ptr[r]; q < tb.row_ptr[r + 1]; ++q)
+            acc += bf.rbuf[((size_t)cw * tb.nT + tb.row_t[q]) * tb.Mr + il];
         out[(size_t)cw * tb.n + i] = acc;
     }
 }
@@ -578,7 +598,7 @@ int amp_launch_control(const AmpTables<T> &tb, const AmpBufs<T> &bf, const AmpSc
                        int phase, int t, hipStream_t s) {
     if (bf.B <= 0) return SG_OK;
     ProfScope ps(SG_PH_CONTROL, s);
-    hipLaunchKernelGGL((control_kernel<T>), dim3(bf.B), dim3(256), 0, s, tb, bf, sc, pr, phase, t);
+    hipLaunchKernelGGL((control_kernel<T>), dim3(bf.B), dim3(1024), 0, s, tb, bf, sc, pr, phase, t);
     SG_HIP(hipGetLastError());
     return SG_OK;
 }

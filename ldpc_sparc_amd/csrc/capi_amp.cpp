@@ -20,7 +20,8 @@ struct sg_amp_plan {
     std::vector<double> W;
     std::vector<void *> allocs;  // every device allocation owned by the plan
     // device tables
-    int32_t *t_row = nullptr, *t_col = nullptr, *col_ptr = nullptr, *col_t = nullptr;
+    int32_t *t_row = nullptr, *t_col = nullptr, *col_ptr = nullptr, *col_t = nullptr, *row_ptr = nullptr,
+            *row_t = nullptr;
     int32_t *inmap = nullptr, *outslot = nullptr, *rp_ptr = nullptr, *rp_i = nullptr;
     uint32_t *rp_ab = nullptr;
     int32_t *gs_ptr = nullptr, *gs_loc = nullptr, *gs_i = nullptr;
@@ -51,6 +52,14 @@ struct sg_amp_plan {
     void *ws_s = nullptr, *ws_tu = nullptr, *ws_xn = nullptr, *ws_part = nullptr, *ws_stM = nullptr,
          *ws_stI = nullptr;
     double *ws_tau_prev = nullptr;
+    // block engine (several transforms per column block, amp_block.hip)
+    bool block = false;
+    uint16_t *b_gloc = nullptr;
+    uint32_t *b_pos2 = nullptr, *b_oab = nullptr;
+    int32_t *b_gptr = nullptr, *b_gi = nullptr, *b_grow = nullptr;
+    int b_ngs = 0;
+    void *ws_gbuf = nullptr;  // [B][b_ngs] G slots (block engine)
+    void *b_oc = nullptr, *b_gc = nullptr, *b_stw = nullptr;
 };
 
 extern "C" int sg_amp_plan_destroy(sg_amp_plan *p);
@@ -144,7 +153,7 @@ static int plan_free_ws(sg_amp_plan *p) {
                    (void **)&p->ws_psi, (void **)&p->ws_psi_prev, (void **)&p->ws_phi_prev, (void **)&p->ws_gamma,
                    (void **)&p->ws_bco, (void **)&p->ws_nmse, (void **)&p->ws_active, (void **)&p->ws_argmax,
                    (void **)&p->ws_true, (void **)&p->ws_tfinal, &p->ws_s, &p->ws_tu, &p->ws_xn, &p->ws_part,
-                   &p->ws_stM, &p->ws_stI, (void **)&p->ws_tau_prev};
+                   &p->ws_stM, &p->ws_stI, (void **)&p->ws_tau_prev, &p->ws_gbuf};
     for (void **x : ws) {
         if (*x) hipFree(*x);
         *x = nullptr;
@@ -186,6 +195,7 @@ static int ensure_ws(sg_amp_plan *p, int B, int t_max) {
         SG_ALLOC(p->ws_sumsq, Bz * p->L * 8);
         SG_ALLOC(p->ws_err, Bz * p->L * 8);
     }
+    if (p->block) SG_ALLOC(p->ws_gbuf, Bz * (size_t)p->b_ngs * 8);
     SG_ALLOC(p->ws_phi, Bz * p->Lr * 8);
     SG_ALLOC(p->ws_tau, Bz * p->Lc * 8);
     SG_ALLOC(p->ws_psi, Bz * p->Lc * 8);
@@ -215,6 +225,20 @@ static AmpTables<T> tables(const sg_amp_plan *p) {
     tb.rp_c = (const cx<T> *)p->rp_c; tb.gs_ptr = p->gs_ptr; tb.gs_loc = p->gs_loc; tb.gs_i = p->gs_i;
     tb.gs_c = (const cx<T> *)p->gs_c; tb.twP = (const cx<T> *)p->twP; tb.twQ = (const cx<T> *)p->twQ;
     tb.twHi = (const cx<T> *)p->twHi; tb.twLo = (const cx<T> *)p->twLo;
+    tb.row_ptr = p->row_ptr; tb.row_t = p->row_t;
+    return tb;
+}
+
+static BlkTables btables(const sg_amp_plan *p) {
+    BlkTables tb;
+    tb.nT = p->nT; tb.L = p->L; tb.M = p->M; tb.LM = p->LM; tb.n = p->n; tb.Lr = p->Lr; tb.Lc = p->Lc;
+    tb.Mr = p->Mr; tb.Mc = p->Mc;
+    tb.col_ptr = p->col_ptr; tb.col_t = p->col_t; tb.t_row = p->t_row;
+    tb.pos2 = p->b_pos2; tb.oab = p->b_oab; tb.oc = (const cx<float> *)p->b_oc;
+    tb.ngs = p->b_ngs; tb.gptr = p->b_gptr; tb.grow = p->b_grow; tb.gloc = p->b_gloc; tb.gi = p->b_gi; tb.gc = (const cx<float> *)p->b_gc;
+    tb.stw = (const cx<float> *)p->b_stw;
+    const char *sk = std::getenv("SG_AMP_SKIP");  // timing ablation only: results are wrong when set
+    tb.skip = sk ? std::atoi(sk) : 0;
     return tb;
 }
 
@@ -495,6 +519,78 @@ static RegBufs<T> rbufs(const sg_amp_plan *p, int B, const void *y) {
     return bf;
 }
 
+// Tables of the block engine (amp_block.hip): per transform, the LDS position
+// of every column entry, the output gathers and the G slots, all in the
+// natural-order FFT image of lds_fft1_ct (fsw positions).
+static int build_block(sg_amp_plan *p, const uint32_t *order0, const uint32_t *order1,
+                       const std::vector<double> &t_scale, const std::vector<int32_t> &row_of) {
+    const long long N = p->w, N2 = p->N2;
+    const int nT = p->nT, Mc = p->Mc, Mr = p->Mr;
+    std::vector<uint16_t> gloc;
+    std::vector<uint32_t> pos2((size_t)nT * 8 * 1024, 0u);
+    std::vector<uint32_t> oab((size_t)nT * Mr);
+    std::vector<cd> oc((size_t)nT * Mr * 2), gc;
+    std::vector<int32_t> gptr(nT + 1, 0), gi, grow;
+    for (int t = 0; t < nT; ++t) {
+        const uint32_t *o0 = order0 + (size_t)t * Mr, *o1 = order1 + (size_t)t * Mc;
+        for (int j = 0; j < Mc; ++j) {
+            const long long sl = slot_of_pos(o1[j], N);
+            const uint32_t lds = (uint32_t)(2 * fsw((int)(sl >> 1)) + (int)(sl & 1));
+            // owner (thread, entry) of column entry j: amp_block.hip bk_j
+            const int M = p->M, eps = M / 64, spw = 1024 / M;
+            const int l = j / M, rr = j % M;
+            const int tid = (l / spw) * 64 + rr / eps, i = (l % spw) * eps + rr % eps;
+            pos2[((size_t)t * 8 + i / 2) * 1024 + tid] |= lds << (16 * (i & 1));
+        }
+        std::vector<std::vector<std::pair<int, cd>>> gcon(N2);
+        for (int i = 0; i < Mr; ++i) {
+            long long a, b;
+            cd c1, c2;
+            fwd_coef(o0[i], N, N2, t_scale[t], &a, &b, &c1, &c2);
+            oab[(size_t)t * Mr + i] = (uint32_t)fsw((int)a) | ((uint32_t)fsw((int)b) << 16);
+            oc[((size_t)t * Mr + i) * 2] = c1;
+            oc[((size_t)t * Mr + i) * 2 + 1] = c2;
+            inv_contrib(o0[i], N, N2, t_scale[t], [&](long long k, cd c) { gcon[k].push_back({i, c}); });
+        }
+        for (int k = 0; k < N2; ++k) {
+            if (gcon[k].empty()) continue;
+            SG_CHECK_ARG(gcon[k].size() <= 4, "internal: >4 contributions to one G slot");
+            gloc.push_back((uint16_t)fsw(k));
+            grow.push_back(row_of[t]);
+            for (int q = 0; q < 4; ++q) {
+                if (q < (int)gcon[k].size()) { gi.push_back(gcon[k][q].first); gc.push_back(gcon[k][q].second); }
+                else { gi.push_back(-1); gc.push_back(cd(0, 0)); }
+            }
+        }
+        gptr[t + 1] = (int32_t)gloc.size();
+    }
+    std::vector<cd> stw;  // per-stage twiddles of the N2-point FFT (fft.hpp lds_fft1_ct, EPT 16)
+    {
+        int radix[8];
+        const int ns = fft1_plan(ilog2((int)N2), 16, radix);
+        int lns = 0;
+        for (int st = 0; st < ns; ++st) {
+            const int R = radix[st];
+            const long long Ns = 1LL << lns;
+            for (long long k = 0; k < Ns; ++k)
+                for (int q = 0; q < tw_per_k(R); ++q) stw.push_back(tw(tw_exp(R, q) * k, Ns * R));
+            lns += ilog2(R);
+        }
+    }
+    SG_TRY(upload(p, &p->b_pos2, pos2));
+    SG_TRY(upload(p, &p->b_oab, oab));
+    SG_TRY(upload_cx(p, &p->b_oc, oc));
+    SG_TRY(upload(p, &p->b_gptr, gptr));
+    SG_TRY(upload(p, &p->b_grow, grow));
+    p->b_ngs = gptr[nT];
+    SG_TRY(upload(p, &p->b_gloc, gloc));
+    SG_TRY(upload(p, &p->b_gi, gi));
+    SG_TRY(upload_cx(p, &p->b_gc, gc));
+    SG_TRY(upload_cx(p, &p->b_stw, stw));
+    SG_CHECK_ARG(blk_lds_bytes(Mc) <= 160 * 1024, "block engine LDS budget");
+    return SG_OK;
+}
+
 static int build_plan(int ndim, const double *W, int Lr_in, int Lc_in, int L, int M, int n, const uint32_t *order0,
                       const uint32_t *order1, int precision, sg_amp_plan **out) {
     SG_CHECK_ARG(out && W && order0 && order1, "null argument");
@@ -537,11 +633,16 @@ static int build_plan(int ndim, const double *W, int Lr_in, int Lc_in, int L, in
         }
     p->nT = (int)t_row.size();
     SG_CHECK_ARG(p->nT > 0, "base matrix is all zero");
-    std::vector<int32_t> col_ptr(Lc + 1, 0), col_t;
+    std::vector<int32_t> col_ptr(Lc + 1, 0), col_t, row_ptr(Lr + 1, 0), row_t;
     for (int c = 0; c < Lc; ++c) {
         for (int t = 0; t < p->nT; ++t)
             if (t_col[t] == c) col_t.push_back(t);
         col_ptr[c + 1] = (int32_t)col_t.size();
+    }
+    for (int r = 0; r < Lr; ++r) {
+        for (int t = 0; t < p->nT; ++t)
+            if (t_row[t] == r) row_t.push_back(t);
+        row_ptr[r + 1] = (int32_t)row_t.size();
     }
     // one transform per column block: the regular engine (amp_fused.hip);
     // SG_AMP_ENGINE=legacy keeps the general four-step path for comparison
@@ -550,6 +651,10 @@ static int build_plan(int ndim, const double *W, int Lr_in, int Lc_in, int L, in
     // beside the stage-1 FFT: at most 2048 (f64) / 4096 (f32) sections)
     const size_t sec_bytes = (size_t)2 * (L / Lc) * (precision == SG_F64 ? 8 : 4);
     p->regular = ndim <= 1 && p->nT == Lc && sec_bytes <= 32 * 1024 && !(eng && std::strcmp(eng, "legacy") == 0);
+    // several transforms per column block, each small enough for one
+    // workgroup's LDS: the block engine (single precision, w = 2^15)
+    p->block = !p->regular && precision == SG_F32 && p->N2 == (1 << 14) && Mc == (1 << 14) && M >= 64 &&
+               M <= 1024 && Mr < 65536 && !(eng && (std::strcmp(eng, "legacy") == 0 || std::strcmp(eng, "general") == 0));
     const int N = w, N2 = p->N2, P = p->P, Q = p->Q, np1 = p->npairs + 1;
     auto slot_of = [&](long long pos) -> long long {  // w-space slot of position pos
         return (pos % 2 == 0) ? pos / 2 : (long long)N - 1 - (pos - 1) / 2;
@@ -638,6 +743,8 @@ static int build_plan(int ndim, const double *W, int Lr_in, int Lc_in, int L, in
     SG_TRY(upload(pp, &pp->t_col, t_col));
     SG_TRY(upload(pp, &pp->col_ptr, col_ptr));
     SG_TRY(upload(pp, &pp->col_t, col_t));
+    SG_TRY(upload(pp, &pp->row_ptr, row_ptr));
+    SG_TRY(upload(pp, &pp->row_t, row_t));
     SG_TRY(upload(pp, &pp->inmap, inmap));
     SG_TRY(upload(pp, &pp->outslot, outslot));
     SG_TRY(upload(pp, &pp->rp_ptr, rp_ptr));
@@ -654,6 +761,7 @@ static int build_plan(int ndim, const double *W, int Lr_in, int Lc_in, int L, in
     SG_TRY(upload_cx(pp, &pp->twLo, twLo));
     SG_TRY(upload(pp, &pp->dW, Wd));
     if (pp->regular) SG_TRY(build_regular(pp, order0, order1, t_scale));
+    if (pp->block) SG_TRY(build_block(pp, order0, order1, t_scale, t_row));
     return SG_OK;
     }();
     if (rc != SG_OK) {
@@ -726,12 +834,24 @@ static int decode_impl(sg_amp_plan *p, const void *d_y, int B, const int32_t *d_
     SG_HIP(hipMemsetAsync(p->ws_beta, 0, (size_t)B * p->LM * rs, s));
     SG_TRY(amp_launch_control<T>(tb, bf, sc, pr, 2, 0, s));
     std::vector<int32_t> act(B);
+    const bool blk = p->block && sizeof(T) == 4;
+    const BlkTables bt = blk ? btables(p) : BlkTables{};
     for (int t = 0; t < t_max - 1; ++t) {
-        if (t > 0) SG_TRY(amp_launch_ab<T>(tb, bf, s));
-        SG_TRY(amp_launch_control<T>(tb, bf, sc, pr, 0, t, s));
-        SG_TRY(amp_launch_az<T>(tb, bf, s));
-        SG_TRY(amp_launch_eta<T>(tb, bf, s));
-        SG_TRY(amp_launch_control<T>(tb, bf, sc, pr, 1, t, s));
+        if constexpr (sizeof(T) == 4) {
+            if (blk) {
+                if (t > 0) SG_TRY(blk_launch_ab(bt, bf, s));
+                SG_TRY(amp_launch_control<T>(tb, bf, sc, pr, 0, t, s));
+                SG_TRY(blk_launch_az(bt, bf, (cx<float> *)p->ws_gbuf, s));
+                SG_TRY(amp_launch_control<T>(tb, bf, sc, pr, 1, t, s));
+            }
+        }
+        if (!blk) {
+            if (t > 0) SG_TRY(amp_launch_ab<T>(tb, bf, s));
+            SG_TRY(amp_launch_control<T>(tb, bf, sc, pr, 0, t, s));
+            SG_TRY(amp_launch_az<T>(tb, bf, s));
+            SG_TRY(amp_launch_eta<T>(tb, bf, s));
+            SG_TRY(amp_launch_control<T>(tb, bf, sc, pr, 1, t, s));
+        }
         if (t % 4 == 3 && t + 1 < t_max - 1) {  // skip the remaining launches once every codeword stopped
             SG_HIP(hipMemcpyAsync(act.data(), p->ws_active, sizeof(int32_t) * B, hipMemcpyDeviceToHost, s));
             SG_HIP(hipStreamSynchronize(s));
