@@ -10,7 +10,9 @@ GPU -- the RCCL all-reduce of the error counters.  Inputs are synthetic
 before the timed region.
 
 Secondary (C3): batched min-sum BP on 802.11n r1/2 z=81 (n=1944), 50
-iterations, 4096 codewords, reported in the "bp" object.
+iterations, 4096 codewords, reported in the "bp" object.  C4 (spatially
+coupled, block engine) in the "sc" object, C5 (concatenated SPARC+LDPC) in
+"concat".
 
 Roofline: the AMP kernels of one iteration against HBM with SURVEY.md 8(d)'s
 algorithmic bytes per codeword-iteration 4*(2LM+4n); the BP kernel with
@@ -56,6 +58,9 @@ def parse():
     ap.add_argument("--bp-steps", type=int, default=10)
     ap.add_argument("--no-bp", action="store_true")
     ap.add_argument("--no-concat", action="store_true")
+    ap.add_argument("--no-sc", action="store_true")
+    ap.add_argument("--sc-batch", type=int, default=256)
+    ap.add_argument("--sc-steps", type=int, default=2)
     ap.add_argument("--concat-batch", type=int, default=256)
     ap.add_argument("--concat-steps", type=int, default=2)
     ap.add_argument("--concat-ebn0", type=float, default=4.0)
@@ -242,6 +247,97 @@ def bp_cpu_baseline(st, seconds):
                       f"{st.get('ebn0')} dB) by oracle/bp_oracle.c on 1 host core"}
 
 
+# ------------------------------------------------------------------ spatially coupled (C4)
+
+def sc_bench(args, d, comm, cpu_seconds):
+    """C4 (BASELINE.json configs[3], sparc_demo_sc_decode_wave): spatially
+    coupled SPARC, omega=6, Lambda=32 (W 37x32, 192 transforms of w=2^15),
+    L=1024, M=512, R=1.5 (n=6142), P=15, sigma^2=1, t_max=40; block engine
+    (amp_block.hip).  Synthetic inputs generated on the GPU as for C2."""
+    L, M, P, omega, Lam, logM = 1024, 512, 15.0, 6, 32, 9
+    W = sparc.sc_basic(np.array(P), omega, Lam)
+    Lr, Lc = W.shape
+    n = int(round(L * logM / args.rate))
+    Mr = int(round(n / Lr))
+    n = Mr * Lr
+    o0, o1 = sparc.generate_ordering(W, Mr, L * M // Lc, 0)
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    plan = op.plan(_native.SG_F32)
+    lib = _native.lib()
+    B, t_max = args.sc_batch, 40
+    d_bits = _native.DeviceBuffer(B * L * logM)
+    d_true = _native.DeviceBuffer(B * L * 4)
+    d_x = _native.DeviceBuffer(B * n * 4)
+    d_y = _native.DeviceBuffer(B * n * 4)
+    _native.check(lib.sg_rng_bits_device(args.seed + 7, d.rank, B, L * logM, d_bits.ptr, None))
+    _native.check(lib.sg_bits_to_sections_device(d_bits.ptr, B, L, logM, d_true.ptr, None))
+    _native.check(lib.sg_amp_encode_device(plan, d_true.ptr, B, d_x.ptr, None))
+    _native.check(lib.sg_awgn_device(_native.SG_F32, args.seed + 7, d.rank, d_x.ptr, B, n, 1.0, d_y.ptr, None))
+    d_map, d_tf, d_cnt = _native.DeviceBuffer(B * L * 4), _native.DeviceBuffer(B * 4), _native.DeviceBuffer(32)
+
+    def step():
+        _native.check(lib.sg_memset(d_cnt.ptr, 0, 32, None))
+        _native.check(lib.sg_amp_decode_device(plan, d_y.ptr, B, d_true.ptr, 1.0, t_max, 1e-6, 1, d_map.ptr,
+                                               d_tf.ptr, None, None, None))
+        _native.check(lib.sg_amp_count_errors_device(d_map.ptr, d_true.ptr, d_tf.ptr, B, L, logM, d_cnt.ptr,
+                                                     None))
+        if comm is not None:
+            comm.allreduce_sum_i64(d_cnt, 4)
+
+    step()
+    _native.device_synchronize()
+    prof = _native.Profiler()
+    d.barrier()
+    _native.device_synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.sc_steps):
+        step()
+    _native.device_synchronize()
+    el = d.max(time.perf_counter() - t0)
+    ph = prof.stop()
+    tf = d_tf.download(np.zeros(B, np.int32))
+    cnt = d_cnt.download(np.zeros(4, np.int64))
+    cw_it = int(tf.sum()) * args.sc_steps
+    kms = sum(ph.get(k, (0.0, 0))[0] for k in AMP_PHASES)
+    w = int(op.w)
+    flops = 2 * int(np.count_nonzero(W)) * 2.5 * w * np.log2(w) + 20 * L * M  # per codeword-iteration
+    ach = flops * cw_it / (kms * 1e-3) / 1e12 if kms else None
+    out = {"workload": "C4: spatially coupled SPARC (omega=6, Lambda=32, W 37x32, 192 transforms of w=2^15), "
+                       f"L=1024, M=512, R={args.rate} (n={n}), P=15, sigma^2=1, t_max=40",
+           "value": d.world * B * args.sc_steps / el, "unit": "codewords/s", "batch_per_gpu": B,
+           "avg_iterations": float(tf.mean()), "section_errors": int(cnt[0]), "codeword_errors": int(cnt[2]),
+           "ser": float(cnt[0]) / (d.world * B * L),
+           "roofline": {"bound": "valu-f32", "achieved": ach, "peak": VALU_PEAK_TFS, "unit": "TFLOP/s",
+                        "frac": ach / VALU_PEAK_TFS if ach else None, "traffic": None,
+                        "kernel": "blk_ab + blk_g + blk_az + control (amp_block.hip)",
+                        "algorithmic_flops_per_codeword_iteration": flops,
+                        "note": "2 nT transforms x 2.5 w log2 w + 20 L M per codeword-iteration; each transform "
+                                "runs in one workgroup's LDS, so HBM sees only beta, z and the tables",
+                        "kernel_ms": {k: round(v[0], 3) for k, v in ph.items()},
+                        "launches": {k: v[1] for k, v in ph.items()}}}
+    if d.rank == 0 and d.world == 1 and cpu_seconds > 0:
+        from oracle import sparc_ref
+        Ab, Az = sparc_ref.dct_operators(W, L, M, n, o0, o1)
+        Y = d_y.download(np.zeros((B, n), np.float32)).astype(np.float64)
+        true = d_true.download(np.zeros((B, L), np.int32))
+        t0 = time.perf_counter()
+        done = iters = 0
+        while True:
+            beta0 = np.zeros(L * M)
+            beta0[np.arange(L) * M + true[done]] = 1.0
+            _, t_f, _, _ = sparc_ref.amp(Y[done], W, L, M, n, 1.0, t_max, Ab, Az, beta0)
+            done += 1
+            iters += t_f
+            cel = time.perf_counter() - t0
+            if cel >= cpu_seconds or done >= B:
+                break
+        out["cpu_baseline"] = {"value": done / cel, "unit": "codewords/s", "cores": 1, "kind": "port",
+                               "sample": f"{done} C4 codewords ({iters} AMP iterations, {cel:.1f} s) decoded by "
+                                         "oracle/sparc_ref.py (scipy fftpack DCT per block, float128 softmax) "
+                                         "on 1 host core"}
+    return out
+
+
 # ------------------------------------------------------------------ concatenated (C5)
 
 MFMA_F32_PEAK_TFS = 157.3  # MI355X f32 MFMA dense peak (MI355X_MICROARCH.md)
@@ -407,6 +503,9 @@ def main():
                                   "kernel": "bp_flood_kernel<float, minsum>",
                                   "algorithmic_bytes_per_codeword_iteration": bbytes,
                                   "kernel_ms": bp_ms, "launches": ph.get("bp_flood", (0, 0))[1]}}
+
+    if not args.no_sc:
+        out["sc"] = sc_bench(args, d, comm, args.cpu_seconds / 2 if d.world == 1 else 0)
 
     if not args.no_concat:
         out["concat"] = concat_bench(args, d)

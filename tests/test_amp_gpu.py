@@ -202,3 +202,61 @@ def test_full_size_decode_f64_vs_oracle():
     assert tf[0] == rt
     np.testing.assert_allclose(nm[0, :, 0], rn, atol=1e-8)
     assert np.mean(mi[0] != np.argmax(rb.reshape(L, M), 1)) < 0.01
+
+
+def _c4_design(seed, R=1.5):
+    """C4 geometry (sparc_demo_sc_decode_wave): spatially coupled omega=6,
+    Lambda=32, L=1024, M=512 -> W 37x32, Mr=166, n=6142, Mc=16384, w=2^15."""
+    L, M, P, omega, Lam = 1024, 512, 15.0, 6, 32
+    W = sparc.sc_basic(np.array(P), omega, Lam)
+    Lr, Lc = W.shape
+    n = int(round(L * 9 / R))
+    Mr = int(round(n / Lr))
+    n = Mr * Lr
+    o0, o1 = sparc.generate_ordering(W, Mr, L * M // Lc, seed)
+    return W, L, M, n, o0, o1
+
+
+def _c4_batch(op, B, seed):
+    rng = np.random.default_rng(seed)
+    true = rng.integers(0, op.M, (B, op.L))
+    beta0 = np.zeros((B, op.L * op.M))
+    beta0[np.arange(B)[:, None], np.arange(op.L) * op.M + true] = 1
+    return op.apply(beta0, False) + rng.standard_normal((B, op.n)), true
+
+
+def test_c4_block_engine_vs_oracle():
+    """One C4 codeword through the f32 block engine (amp_block.hip) against
+    the CPU restatement (float128 softmax): t_final within +-2, the same MAP
+    decisions on all but 0.5 % of the sections, NMSE within 2e-3 over the
+    first 10 iterations (f32 bar of the module docstring)."""
+    W, L, M, n, o0, o1 = _c4_design(5)
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    assert op.w == 2 ** 15 and W.shape == (37, 32)
+    Ab, Az = sparc_ref.dct_operators(W, L, M, n, o0, o1)
+    rng = np.random.RandomState(6)
+    true = rng.randint(0, M, L)
+    beta0 = np.zeros(L * M)
+    beta0[np.arange(L) * M + true] = 1
+    y = Ab(beta0) + rng.randn(n)
+    rb, rt, rn, rp = sparc_ref.amp(y, W, L, M, n, 1.0, 40, Ab, Az, beta0)
+    mi, tf, nm, ps = sparc.amp_decode_batch(y[None], op, 1.0, 40, true_idx=true[None], precision=_native.SG_F32)
+    assert abs(int(tf[0]) - int(rt)) <= 2, (tf[0], rt)
+    assert np.mean(mi[0] != np.argmax(rb.reshape(L, M), 1)) < 0.005
+    np.testing.assert_allclose(nm[0, :10], np.asarray(rn).reshape(40, -1)[:10], atol=2e-3)
+
+
+def test_c4_block_engine_vs_general_engine(monkeypatch):
+    """The block engine and the general four-step engine (SG_AMP_ENGINE=general)
+    decode the same C4 batch to the same decisions and stopping iterations."""
+    W, L, M, n, o0, o1 = _c4_design(7)
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    Y, true = _c4_batch(op, 8, 9)
+    mb, tb_, nb, _ = sparc.amp_decode_batch(Y, op, 1.0, 40, true_idx=true, precision=_native.SG_F32)
+    monkeypatch.setenv("SG_AMP_ENGINE", "general")
+    og = sparc.DesignOperator(W, L, M, n, o0, o1)
+    mg, tg, ng, _ = sparc.amp_decode_batch(Y, og, 1.0, 40, true_idx=true, precision=_native.SG_F32)
+    assert np.all(np.abs(tb_ - tg) <= 1)
+    assert np.mean(mb != mg) < 1e-3
+    np.testing.assert_allclose(nb[:, :10], ng[:, :10], atol=1e-4)
+    assert np.mean(mb != true) < 0.05  # the decode wave runs through at R = 1.5
