@@ -38,8 +38,9 @@ struct BlkTables {
     const int32_t *col_ptr, *col_t, *t_row;
     const uint32_t *pos2;     // [nT][8][1024] real LDS index (2 fsw(m) + component) of column entry
                               // j = tid + 1024 i, pairs (i = 2 i2, 2 i2 + 1) at [t][i2][tid]
-    const uint32_t *oab;      // [nT][Mr] fsw(a) | fsw(b) << 16 of output i
-    const cx<float> *oc;      // [nT][Mr][2] X_i = Re(c1 H[a] + c2 conj H[b])
+    const uint32_t *oab;      // [nT][Mr] (a mod 4096) | (b mod 4096) << 16 of output i
+    const cx<float> *oc;      // [nT][Mr][8] X_i = Re(sum_r al_r Y[a mod 4096 + 4096 r] + be_r conj Y[b mod ...]),
+                              // al_r = c1 w_N2^(r a), be_r = c2 conj w_N2^(r b) (the last FFT stage folded in)
     int ngs;                  // G slots of all transforms (= gptr[nT])
     const int32_t *gptr;      // [nT + 1] G slots of each transform (CSR)
     const int32_t *grow;      // row block of each slot's transform

@@ -86,6 +86,18 @@ __device__ __forceinline__ void bk_pos_load(const BlkTables &tb, int t, int tid,
 }
 __device__ __forceinline__ uint32_t bk_pos(const uint32_t *pv, int i) { return (pv[i >> 1] >> (16 * (i & 1))) & 0xffffu; }
 
+// The first three stages of the 2^14-point FFT of fft.hpp (radix 16, 16, 16,
+// then 4; stage twiddles tb.stw as lds_fft1_ct): the forward transform stops
+// before the radix-4 stage, which blk_ab folds into the needed outputs.
+__device__ __forceinline__ void bk_fwd_stages(cx<float> *d, const cx<float> *__restrict__ stw, int tid) {
+    cx<float> w0[1], w1[6], w2[6];
+    fft1_tw_load_ct<float, 16, BK_LOG2N, 1>(stw, tid, w1);
+    stockham1_stage_ct<float, false, 16, 16, BK_LOG2N, 0>(d, w0, tid);
+    fft1_tw_load_ct<float, 16, BK_LOG2N, 2>(stw, tid, w2);
+    stockham1_stage_ct<float, false, 16, 16, BK_LOG2N, 4>(d, w1, tid);
+    stockham1_stage_ct<float, false, 16, 16, BK_LOG2N, 8>(d, w2, tid);
+}
+
 // ------------------------------------------------------------------ Ab
 template <int EPS>
 __global__ __launch_bounds__(BK_THREADS) void blk_ab(BlkTables tb, AmpBufs<float> bf) {
@@ -112,15 +124,24 @@ __global__ __launch_bounds__(BK_THREADS) void blk_ab(BlkTables tb, AmpBufs<float
         for (int i = 0; i < BK_J; ++i)
             dr[bk_pos(pv, i)] = bv[i];
         __syncthreads();
-        lds_fft1_ct<float, false, 16, BK_LOG2N>(d, tb.stw, tl);
+        bk_fwd_stages(d, tb.stw, tl);
+        // the last (radix-4, Ns = 4096) stage only for the needed bins, folded
+        // into the outputs: H[a] = sum_r Y[a mod 4096 + 4096 r] w_N2^(r a), so
+        // X_i = Re(c1 H[a] + c2 conj H[b]) = Re(sum_r al_r Y_a,r + be_r conj Y_b,r)
         float *r = bf.rbuf + ((size_t)cw * tb.nT + t) * tb.Mr;
         const uint32_t *oab = tb.oab + (size_t)t * tb.Mr;
-        const cx<float> *oc = tb.oc + (size_t)t * tb.Mr * 2;
+        const cx<float> *oc = tb.oc + (size_t)t * tb.Mr * 8;
         for (int i = tl; i < tb.Mr; i += BK_THREADS) {
             const uint32_t ab = oab[i];
-            const cx<float> ha = d[ab & 0xffffu], hb = d[ab >> 16];
-            const cx<float> c1 = oc[2 * i], c2 = oc[2 * i + 1];
-            r[i] = (c1.x * ha.x - c1.y * ha.y) + (c2.x * hb.x + c2.y * hb.y);  // Re(c1 ha + c2 conj hb)
+            const int ja = ab & 0xffffu, jb = ab >> 16;
+            float acc = 0.f;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const cx<float> ya = d[fsw(ja + 4096 * q)], yb = d[fsw(jb + 4096 * q)];
+                const cx<float> al = oc[8 * i + q], be = oc[8 * i + 4 + q];
+                acc += (al.x * ya.x - al.y * ya.y) + (be.x * yb.x + be.y * yb.y);
+            }
+            r[i] = acc;
         }
         __syncthreads();
     }

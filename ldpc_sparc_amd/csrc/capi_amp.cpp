@@ -529,7 +529,7 @@ static int build_block(sg_amp_plan *p, const uint32_t *order0, const uint32_t *o
     std::vector<uint16_t> gloc;
     std::vector<uint32_t> pos2((size_t)nT * 8 * 1024, 0u);
     std::vector<uint32_t> oab((size_t)nT * Mr);
-    std::vector<cd> oc((size_t)nT * Mr * 2), gc;
+    std::vector<cd> oc((size_t)nT * Mr * 8), gc;
     std::vector<int32_t> gptr(nT + 1, 0), gi, grow;
     for (int t = 0; t < nT; ++t) {
         const uint32_t *o0 = order0 + (size_t)t * Mr, *o1 = order1 + (size_t)t * Mc;
@@ -547,9 +547,12 @@ static int build_block(sg_amp_plan *p, const uint32_t *order0, const uint32_t *o
             long long a, b;
             cd c1, c2;
             fwd_coef(o0[i], N, N2, t_scale[t], &a, &b, &c1, &c2);
-            oab[(size_t)t * Mr + i] = (uint32_t)fsw((int)a) | ((uint32_t)fsw((int)b) << 16);
-            oc[((size_t)t * Mr + i) * 2] = c1;
-            oc[((size_t)t * Mr + i) * 2 + 1] = c2;
+            // amp_block.hip blk_ab: the radix-4 stage of bins a, b folded into the output
+            oab[(size_t)t * Mr + i] = (uint32_t)(a % 4096) | ((uint32_t)(b % 4096) << 16);
+            for (int q = 0; q < 4; ++q) {
+                oc[((size_t)t * Mr + i) * 8 + q] = c1 * tw((long long)q * a, N2);
+                oc[((size_t)t * Mr + i) * 8 + 4 + q] = c2 * std::conj(tw((long long)q * b, N2));
+            }
             inv_contrib(o0[i], N, N2, t_scale[t], [&](long long k, cd c) { gcon[k].push_back({i, c}); });
         }
         for (int k = 0; k < N2; ++k) {
