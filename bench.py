@@ -182,22 +182,36 @@ def amp_cpu_baseline(st, args, seconds):
     dt = np.float32 if st["prec"] == _native.SG_F32 else np.float64
     Y = st["d_y"].download(np.zeros((st["B"], n), dt)).astype(np.float64)
     true = st["d_true"].download(np.zeros((st["B"], L), np.int32))
+    gmap = st["d_map"].download(np.zeros((st["B"], L), np.int32))  # the GPU's decisions, same codewords
     t0 = time.perf_counter()
     done = iters = 0
+    cbits = gbits = csec = gsec = same = 0
     while True:
         b = done
         beta0 = np.zeros(L * M)
         beta0[np.arange(L) * M + true[b]] = 1.0
-        _, tf, _, _ = sparc_ref.amp(Y[b], st["W"], L, M, n, 1.0, args.t_max, Ab, Az, beta0)
+        bh, tf, _, _ = sparc_ref.amp(Y[b], st["W"], L, M, n, 1.0, args.t_max, Ab, Az, beta0)
+        cidx = np.argmax(bh.reshape(L, M), 1)
+        cbits += int(sum(bin(int(v)).count("1") for v in (cidx ^ true[b])))
+        gbits += int(sum(bin(int(v)).count("1") for v in (gmap[b] ^ true[b])))
+        csec += int((cidx != true[b]).sum())
+        gsec += int((gmap[b] != true[b]).sum())
+        same += int((cidx == gmap[b]).sum())
         done += 1
         iters += tf
         el = time.perf_counter() - t0
         if el >= seconds or done >= st["B"]:
             break
+    nb = done * L * st["logM"]
     return {"value": done / el, "unit": "codewords/s", "cores": 1, "kind": "port",
             "sample": f"{done} C2 codewords (R={args.rate}, t_max={args.t_max}, {iters} AMP "
                       f"iterations, {el:.1f} s) decoded by oracle/sparc_ref.py (numpy/scipy "
-                      f"fftpack DCT, float128 softmax) on 1 host core"}
+                      f"fftpack DCT, float128 softmax) on 1 host core",
+            "ber_match": {"codewords": done, "cpu_ber": cbits / nb, "gpu_ber": gbits / nb,
+                          "cpu_ser": csec / (done * L), "gpu_ser": gsec / (done * L),
+                          "identical_section_decisions": same / (done * L),
+                          "note": "the GPU's decisions for the same received words (f32 engine vs the f64/"
+                                  "float128 CPU restatement)"}}
 
 
 # ------------------------------------------------------------------ BP (C3)
@@ -233,18 +247,32 @@ def bp_cpu_baseline(st, seconds):
     corrected) on one host core."""
     from oracle import bp
     c = st["c"]
+    gapp = st["d_app"].download(np.zeros((st["B"], c.N), np.float32))  # the GPU's output, same codewords
     t0 = time.perf_counter()
     done = 0
+    cerr = gerr = cfe = gfe = same = 0
     while True:
         chunk = st["ch"][done:done + 64]
-        bp.decode_batch("minsum", chunk, c.vdeg, c.cdeg, c.intrlv, 50, 0.7)
+        app, _ = bp.decode_batch("minsum", chunk, c.vdeg, c.cdeg, c.intrlv, 50, 0.7)
+        x = st["X"][done:done + len(chunk)]
+        ch_, gh = (app < 0).astype(np.int64), (gapp[done:done + len(chunk)] < 0).astype(np.int64)
+        cerr += int((ch_[:, :c.K] != x[:, :c.K]).sum())
+        gerr += int((gh[:, :c.K] != x[:, :c.K]).sum())
+        cfe += int((ch_[:, :c.K] != x[:, :c.K]).any(1).sum())
+        gfe += int((gh[:, :c.K] != x[:, :c.K]).any(1).sum())
+        same += int((ch_ == gh).all(1).sum())
         done += len(chunk)
         el = time.perf_counter() - t0
         if el >= seconds or done >= st["B"]:
             break
     return {"value": done / el, "unit": "codewords/s", "cores": 1, "kind": "port",
             "sample": f"{done} C3 codewords (802.11n r1/2 z=81, min-sum, 50 it, Eb/N0 "
-                      f"{st.get('ebn0')} dB) by oracle/bp_oracle.c on 1 host core"}
+                      f"{st.get('ebn0')} dB) by oracle/bp_oracle.c on 1 host core",
+            "ber_match": {"codewords": done, "cpu_ber": cerr / (done * c.K), "gpu_ber": gerr / (done * c.K),
+                          "cpu_fer": cfe / done, "gpu_fer": gfe / done,
+                          "identical_codeword_decisions": same / done,
+                          "note": "information-bit errors of the GPU (f32) and the CPU restatement (f64) on the same "
+                                  "channel LLRs"}}
 
 
 # ------------------------------------------------------------------ spatially coupled (C4)
