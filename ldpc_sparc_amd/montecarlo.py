@@ -224,6 +224,70 @@ class SparcTrial:
         return np.array([B, cnt[1], cnt[2], cnt[3], cnt[0]], dtype=np.int64)
 
 
+class ConcatTrial:
+    """Concatenated SPARC + LDPC codewords (sparc_sim_new.sparc_ldpc_sim,
+    sparc_new.py:15-82) at the points' AWGN variances,
+    generated and decoded in batches by pipeline.ConcatPipeline (dense AMP ->
+    glue -> batched BP -> device counters).  Block b of point p draws its user
+    bits and noise from default_rng([seed, p, b]), so results do not depend on
+    the rank count.  Counters [codewords, user-bit errors, codeword errors,
+    unprotected-bit errors, protected-bit errors]; per-block BERs of this
+    rank are kept in block_ber[point]."""
+
+    def __init__(self, pipe, awgn_vars, seed=0):
+        self.pipe, self.vars, self.seed = pipe, list(awgn_vars), int(seed)
+        self.user_bits = pipe.L_unp * pipe.logM + pipe.mults * pipe.c.K
+        self.block_ber = {}
+
+    def __call__(self, point, first_block, n_blocks, block):
+        tot = np.zeros(NC, dtype=np.int64)
+        for b in range(first_block, first_block + n_blocks):
+            self.pipe.make_batch(block, self.vars[point], np.random.default_rng([self.seed, int(point), int(b)]))
+            self.pipe.reset_counts()
+            self.pipe.decode()
+            c = self.pipe.counts()
+            tot += c
+            self.block_ber.setdefault(point, []).append(float(c[1]) / (c[0] * self.user_bits))
+        return tot
+
+
+def concat_ber_sweep(L, M, n, P, L_unprotected, mults, ebn0_db, *, codewords, block=256, blocks_per_round=None,
+                     rank=0, world=1, agg=None, design_seed=0, seed=0, t_max=25, bp_its=200, precision="f32",
+                     ldpc=("802.11n", "1/2", 81), min_errors=None, checkpoint_dir=None, npz_file=None):
+    """BER / FER of concatenated SPARC + LDPC against Eb/N0 (the experiment of
+    ldpc_sparc/performance_plots_general.py:100-138 for the plain concatenated
+    decoder), `codewords` per point sharded over the ranks.  Eb/N0 to noise as
+    the bench: awgn_var = P / (2 R_overall 10^(Eb/N0 / 10)), R_overall = user
+    bits / n.  Returns one dict per point; rank 0 writes `npz_file` in the
+    layout of performance_plots_general.py:138 (ber_store_averages, _max,
+    _min over the blocks rank 0 decoded, and snr_store = Eb/N0 in dB)."""
+    from .pipeline import ConcatPipeline
+    agg = agg or Aggregator()
+    pipe = ConcatPipeline(L, M, n, P, L_unprotected, mults, ldpc=ldpc, design_seed=design_seed,
+                          precision=precision, t_max=t_max, bp_its=bp_its)
+    user_bits = L_unprotected * pipe.logM + mults * pipe.c.K
+    r_overall = user_bits / n
+    vars_ = [P / (2 * r_overall * 10 ** (e / 10)) for e in ebn0_db]
+    trial = ConcatTrial(pipe, vars_, seed)
+    bpr = blocks_per_round or max(1, world)
+    out = []
+    for point, e in enumerate(ebn0_db):
+        tot = run_point(trial, point, block=block, blocks_per_round=bpr, rank=rank, world=world, agg=agg,
+                        min_errors=min_errors, max_units=codewords, checkpoint_dir=checkpoint_dir,
+                        tag=f"concat_L{L}_M{M}_n{n}")
+        out.append({"ebn0_db": float(e), "awgn_var": vars_[point], "codewords": int(tot[0]),
+                    "ber": float(tot[1]) / (tot[0] * user_bits) if tot[0] else None,
+                    "fer": float(tot[2]) / tot[0] if tot[0] else None,
+                    "unprotected_bit_errors": int(tot[3]), "protected_bit_errors": int(tot[4]),
+                    "R_overall": r_overall})
+    if npz_file and rank == 0:
+        avg = np.array([[o["ber"] for o in out]], dtype=float)
+        bb = [trial.block_ber.get(p, [np.nan]) for p in range(len(ebn0_db))]
+        np.savez(npz_file, ber_store_averages=avg, ber_store_max=np.array([[np.max(b) for b in bb]]),
+                 ber_store_min=np.array([[np.min(b) for b in bb]]), snr_store=np.asarray(ebn0_db, dtype=float))
+    return out
+
+
 def ldpc_awgn_campaign(standard, rate, z, ptype="A", *, rank=0, world=1, agg=None, N_MEASUREMENTS=24,
                        C_AWGN_OFFSET=1.0, P_STEP=100.0, MIN_ERRORS=100, MAX_BLOCKS=400000, block=256,
                        blocks_per_round=16, dectype="sumprod2", max_it=200, precision="f32", seed=0,

@@ -47,3 +47,23 @@ def test_bp_statistics_match_reference_campaign():
     assert abs(tot[3] / n - 59425 / 1653) < 3.0  # mean reported iteration index
     ber_ref = 16568 / (1653 * c.N)
     assert abs(be / (n * c.N) - ber_ref) < 0.35 * ber_ref
+
+
+def test_concat_sweep_rank_invariant():
+    """C5 sweep on a small concatenated code (L=80, M=512 -> 1 x LDPC z=27 in 72
+    protected sections): the per-point counters do not depend on how the
+    blocks were dealt (two simulated ranks vs one), and BER falls with Eb/N0."""
+    from ldpc_sparc_amd import montecarlo
+    kw = dict(codewords=96, block=32, design_seed=3, seed=4, t_max=10, bp_its=50, ldpc=("802.11n", "1/2", 27))
+    one = montecarlo.concat_ber_sweep(80, 512, 600, 15.0, 8, 1, [1.0, 6.0], **kw)
+    # the same blocks in two shards, summed by hand
+    from ldpc_sparc_amd.pipeline import ConcatPipeline
+    pipe = ConcatPipeline(80, 512, 600, 15.0, 8, 1, ldpc=("802.11n", "1/2", 27), design_seed=3, t_max=10, bp_its=50)
+    ub = 8 * 9 + pipe.c.K
+    for p, e in enumerate([1.0, 6.0]):
+        var = 15.0 / (2 * (ub / 600) * 10 ** (e / 10))
+        tr = montecarlo.ConcatTrial(pipe, [var] * 2, seed=4)
+        a = tr(p, 0, 1, 32) + tr(p, 1, 2, 32)
+        assert int(a[0]) == one[p]["codewords"] == 96
+        assert abs(float(a[1]) / (96 * ub) - one[p]["ber"]) < 1e-12
+    assert one[1]["ber"] <= one[0]["ber"]
