@@ -123,55 +123,92 @@ __device__ __forceinline__ bool check_update(T *__restrict__ msg, int c, int nc,
     return unsat;
 }
 
-template <typename T, int KIND, int MAXDC>
-__global__ __launch_bounds__(BP_THREADS) void bp_flood_kernel(BpArgs<T> a) {
+// LDS image of one workgroup: the messages of its current codeword and --
+// loaded once per workgroup -- the graph tables as 16-bit indices, so the
+// per-iteration passes never leave LDS.  The channel LLRs and the app of the
+// thread's variables (v = tid + BP_THREADS j) stay in registers.
+template <typename T>
+size_t bp_lds_bytes(int slots, int nv, int nports, int nc) {
+    size_t b = sizeof(T) * (size_t)slots;
+    b += sizeof(uint16_t) * ((size_t)nports + nv + 1) + nc;
+    return (b + 15) / 16 * 16;
+}
+
+// waves per SIMD the register allocation must allow: three 512-thread
+// workgroups per CU (80 VGPRs) for single-precision min-sum, whose LDS image
+// of an 802.11n z=81 graph is 50 KB; two (128 VGPRs) for the rest, whose
+// transcendental check nodes would spill at 80
+template <typename T, int KIND>
+constexpr int bp_waves_per_simd() { return (sizeof(T) == 4 && KIND == SG_MINSUM) ? 6 : 4; }
+
+template <typename T, int KIND, int MAXDC, int VJ>
+__global__ __launch_bounds__(BP_THREADS, (bp_waves_per_simd<T, KIND>())) void bp_flood_kernel(BpArgs<T> a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T *msg = reinterpret_cast<T *>(smem);
-    T *app = msg + a.slots;
+    uint16_t *ps = reinterpret_cast<uint16_t *>(msg + a.slots);  // variable port -> message slot
+    uint16_t *vo = ps + a.nports;                                // variable-port offsets
+    uint8_t *cd = reinterpret_cast<uint8_t *>(vo + a.nv + 1);    // check degrees
     const int tid = threadIdx.x;
+    for (int i = tid; i < a.nports; i += BP_THREADS) ps[i] = (uint16_t)a.port_slot[i];
+    for (int i = tid; i <= a.nv; i += BP_THREADS) vo[i] = (uint16_t)a.voff[i];
+    for (int i = tid; i < a.nc; i += BP_THREADS) cd[i] = a.cdeg[i];
     for (int cw = blockIdx.x; cw < a.B; cw += gridDim.x) {
         const T *ch = a.ch + (size_t)cw * a.nv;
+        T chv[VJ], apv[VJ];
+#pragma unroll
+        for (int j = 0; j < VJ; ++j) {
+            const int v = tid + j * BP_THREADS;
+            chv[j] = v < a.nv ? ch[v] : T(0);
+            apv[j] = T(0);
+        }
         for (int i = tid; i < a.slots; i += BP_THREADS) msg[i] = T(0);
         __syncthreads();
         int it = 0;
         for (; it < a.max_it; ++it) {
             // ---- variable pass (c_ldpc.c:171-178)
-            for (int v = tid; v < a.nv; v += BP_THREADS) {
-                const int p0 = a.voff[v];
-                const int d = a.voff[v + 1] - p0;
-                T acc = ch[v];
+#pragma unroll
+            for (int j = 0; j < VJ; ++j) {
+                const int v = tid + j * BP_THREADS;
+                if (v >= a.nv) continue;
+                const int p0 = vo[v];
+                const int d = vo[v + 1] - p0;
+                T acc = chv[j];
                 int s[BP_MAXDV];
                 T m[BP_MAXDV];
 #pragma unroll
                 for (int k = 0; k < BP_MAXDV; ++k)
-                    if (k < d) { s[k] = a.port_slot[p0 + k]; m[k] = msg[s[k]]; acc += m[k]; }
-                for (int k = BP_MAXDV; k < d; ++k) acc += msg[a.port_slot[p0 + k]];
+                    if (k < d) { s[k] = ps[p0 + k]; m[k] = msg[s[k]]; acc += m[k]; }
+                for (int k = BP_MAXDV; k < d; ++k) acc += msg[ps[p0 + k]];
 #pragma unroll
                 for (int k = 0; k < BP_MAXDV; ++k)
                     if (k < d) msg[s[k]] = acc - m[k];
                 for (int k = BP_MAXDV; k < d; ++k) {
-                    const int sl = a.port_slot[p0 + k];
+                    const int sl = ps[p0 + k];
                     msg[sl] = acc - msg[sl];
                 }
-                app[v] = acc;
+                apv[j] = acc;
             }
             __syncthreads();
             // ---- check pass (c_ldpc.c:183-194)
             int unsat = 0;
             for (int c = tid; c < a.nc; c += BP_THREADS)
-                unsat |= check_update<T, KIND, MAXDC>(msg, c, a.nc, a.cdeg[c], a.factor) ? 1 : 0;
+                unsat |= check_update<T, KIND, MAXDC>(msg, c, a.nc, cd[c], a.factor) ? 1 : 0;
             if (!__syncthreads_or(unsat)) break;  // c_ldpc.c:196-197
         }
         T *out = a.app + (size_t)cw * a.nv;
-        for (int v = tid; v < a.nv; v += BP_THREADS) out[v] = app[v];
+#pragma unroll
+        for (int j = 0; j < VJ; ++j) {
+            const int v = tid + j * BP_THREADS;
+            if (v < a.nv) out[v] = apv[j];
+        }
         if (tid == 0) a.it[cw] = it;
         __syncthreads();
     }
 }
 
-template <typename T, int KIND, int MAXDC>
+template <typename T, int KIND, int MAXDC, int VJ>
 static int launch_one(const BpArgs<T> &a, size_t lds, hipStream_t s) {
-    auto kern = bp_flood_kernel<T, KIND, MAXDC>;
+    auto kern = bp_flood_kernel<T, KIND, MAXDC, VJ>;
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BP_THREADS, lds) != hipSuccess || per_cu < 1)
         per_cu = 1;
@@ -185,18 +222,28 @@ static int launch_one(const BpArgs<T> &a, size_t lds, hipStream_t s) {
     return SG_OK;
 }
 
+// variables per thread: 4 (nv <= 2048, every 802.11n code) or BP_VJ
+template <typename T, int KIND, int MAXDC>
+static int dispatch_vj(const BpArgs<T> &a, size_t lds, hipStream_t s) {
+    if (a.nv <= 4 * BP_THREADS) return launch_one<T, KIND, MAXDC, 4>(a, lds, s);
+    return launch_one<T, KIND, MAXDC, BP_VJ>(a, lds, s);
+}
+
 template <typename T, int KIND>
 static int dispatch_dc(const BpArgs<T> &a, int max_cdeg, size_t lds, hipStream_t s) {
-    if (max_cdeg <= 8) return launch_one<T, KIND, 8>(a, lds, s);
-    if (max_cdeg <= 16) return launch_one<T, KIND, 16>(a, lds, s);
-    if (max_cdeg <= 24) return launch_one<T, KIND, 24>(a, lds, s);
-    if (max_cdeg <= 32) return launch_one<T, KIND, 32>(a, lds, s);
+    if (max_cdeg <= 8) return dispatch_vj<T, KIND, 8>(a, lds, s);
+    if (max_cdeg <= 16) return dispatch_vj<T, KIND, 16>(a, lds, s);
+    if (max_cdeg <= 24) return dispatch_vj<T, KIND, 24>(a, lds, s);
+    if (max_cdeg <= 32) return dispatch_vj<T, KIND, 32>(a, lds, s);
     return fail(SG_ERR_UNSUPPORTED, "check degree %d exceeds the supported maximum of 32", max_cdeg);
 }
 
 template <typename T>
 int bp_launch(const BpArgs<T> &a, int dectype, int max_cdeg, hipStream_t s) {
-    const size_t lds = sizeof(T) * ((size_t)a.slots + (size_t)a.nv);
+    const size_t lds = bp_lds_bytes<T>(a.slots, a.nv, a.nports, a.nc);
+    if (a.slots > 65536 || a.nports > 65535 || a.nv > BP_VJ * BP_THREADS)
+        return fail(SG_ERR_UNSUPPORTED, "graph with %d variables / %d message slots / %d ports exceeds the decoder's "
+                    "16-bit LDS tables or %d variables", a.nv, a.slots, a.nports, BP_VJ * BP_THREADS);
     if (lds > BP_MAX_LDS)
         return fail(SG_ERR_UNSUPPORTED,
                     "graph needs %zu B of LDS per codeword (> %d B): too large for the LDS-resident decoder",

@@ -4,8 +4,9 @@
 
 namespace sg {
 
-constexpr int BP_THREADS = 256;
+constexpr int BP_THREADS = 512;
 constexpr int BP_MAXDV = 12;            // variable degrees above this take a slower loop
+constexpr int BP_VJ = 8;                // variables per thread held in registers (nv <= BP_VJ * BP_THREADS)
 constexpr int BP_MAX_LDS = 160 * 1024;  // one workgroup's LDS limit on gfx950
 
 template <typename T>
@@ -14,6 +15,7 @@ struct BpArgs {
     const int32_t *port_slot;  // [nmsg] variable port -> LDS message slot (k*nc + c)
     const uint8_t *cdeg;       // [nc]
     int nv, nc, slots;         // slots = max_cdeg * nc
+    int nports;                // variable ports = edges (voff[nv])
     const T *ch;               // [B][nv]
     T *app;                    // [B][nv]
     int32_t *it;               // [B]

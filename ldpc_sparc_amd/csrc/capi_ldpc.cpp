@@ -87,7 +87,7 @@ static BpArgs<T> make_args(sg_graph *g, const void *ch, int B, int max_it, doubl
     a.voff = g->d_voff;
     a.port_slot = g->d_port_slot;
     a.cdeg = g->d_cdeg;
-    a.nv = g->nv; a.nc = g->nc; a.slots = g->slots;
+    a.nv = g->nv; a.nc = g->nc; a.slots = g->slots; a.nports = g->nmsg;
     a.ch = (const T *)ch;
     a.app = (T *)app;
     a.it = it;
