@@ -42,7 +42,7 @@ from ldpc_sparc_amd.ldpc import code  # noqa: E402
 METRIC = "codewords/sec (AMP+BP) at L=1024 M=512 / n=1944; BER match vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 VALU_PEAK_TFS = 157.3  # MI355X f32 vector peak (packed FMA), MI355X_MICROARCH.md
-AMP_PHASES = ("ab_passA", "ab_passB", "az_passA", "az_passB", "eta", "control")
+AMP_PHASES = ("ab_passA", "ab_passB", "az_passA", "az_passB", "eta", "control", "amp_iter")
 
 
 def parse():
@@ -59,6 +59,7 @@ def parse():
     ap.add_argument("--no-bp", action="store_true")
     ap.add_argument("--no-concat", action="store_true")
     ap.add_argument("--no-sc", action="store_true")
+    ap.add_argument("--no-r13", action="store_true", help="skip the decodable-rate (R=1.3) C2 companion line")
     ap.add_argument("--sc-batch", type=int, default=256)
     ap.add_argument("--sc-steps", type=int, default=2)
     ap.add_argument("--concat-batch", type=int, default=256)
@@ -130,10 +131,10 @@ class HostCounterComm:
 
 # ------------------------------------------------------------------ AMP (C2)
 
-def amp_setup(args, rank):
+def amp_setup(args, rank, rate=None):
     L, M = 1024, 512
     logM = 9
-    n = int(round(L * logM / args.rate))
+    n = int(round(L * logM / (rate or args.rate)))
     W = np.array(15.0)
     prec = _native.SG_F32 if args.precision == "f32" else _native.SG_F64
     o0, o1 = sparc.generate_ordering(W, n, L * M, 0)  # one design shared by every rank
@@ -170,6 +171,34 @@ def amp_step(st, args, comm):
                                                  st["B"], st["L"], st["logM"], st["d_cnt"].ptr, None))
     if comm is not None:
         comm.allreduce_sum_i64(st["d_cnt"], 4)
+
+
+def amp_decodable(args, d, comm, cpu_seconds):
+    """SURVEY.md 8(d) C2 companion: the same engine at R=1.3 (n=7089), where AMP
+    decodes in 14-18 iterations, so the BER comparison with the CPU
+    restatement is made on codewords that mostly decode."""
+    rate = 1.3
+    st = amp_setup(args, d.rank, rate)
+    a = argparse.Namespace(**{**vars(args), "rate": rate})
+    amp_step(st, a, comm)
+    _native.device_synchronize()
+    d.barrier()
+    t0 = time.perf_counter()
+    steps = max(1, args.steps // 2)
+    for _ in range(steps):
+        amp_step(st, a, comm)
+    _native.device_synchronize()
+    el = d.max(time.perf_counter() - t0)
+    cnt = st["d_cnt"].download(np.zeros(4, np.int64))
+    tf = st["d_tf"].download(np.zeros(st["B"], np.int32))
+    out = {"workload": f"C2 at R={rate}: L=1024, M=512, n={st['n']}, same design family, t_max={args.t_max}",
+           "value": d.world * st["B"] * steps / el, "unit": "codewords/s", "batch_per_gpu": st["B"],
+           "avg_iterations": float(tf.mean()), "section_errors": int(cnt[0]), "bit_errors": int(cnt[1]),
+           "codeword_errors": int(cnt[2]),
+           "ber": float(cnt[1]) / (d.world * st["B"] * st["L"] * st["logM"])}
+    if cpu_seconds > 0:
+        out["cpu_baseline"] = amp_cpu_baseline(st, a, cpu_seconds)
+    return out
 
 
 def amp_cpu_baseline(st, args, seconds):
@@ -498,6 +527,9 @@ def main():
                 "bit_errors": int(cnt[1]), "codeword_errors": int(cnt[2]),
                 "ber": float(cnt[1]) / (d.world * st["B"] * st["L"] * st["logM"])},
     }
+
+    if not args.no_r13:
+        out["amp_r13"] = amp_decodable(args, d, comm, args.cpu_seconds / 2 if d.world == 1 and d.rank == 0 else 0)
 
     if not args.no_bp:
         bst = bp_setup(args, d.rank)

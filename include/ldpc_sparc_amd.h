@@ -71,7 +71,7 @@ int sg_device_synchronize(void);
  * launch count per phase (arrays of SG_PH_COUNT) and resets the counters. */
 enum sg_phase {
     SG_PH_AB_A = 0, SG_PH_AB_B = 1, SG_PH_AZ_A = 2, SG_PH_AZ_B = 3, SG_PH_ETA = 4,
-    SG_PH_CONTROL = 5, SG_PH_BP = 6, SG_PH_DENSE = 7, SG_PH_COUNT = 8
+    SG_PH_CONTROL = 5, SG_PH_BP = 6, SG_PH_DENSE = 7, SG_PH_AMP_CW = 8, SG_PH_COUNT = 9
 };
 int sg_profile_enable(int on);
 int sg_profile_collect(double *total_ms, int64_t *launches);
@@ -262,6 +262,11 @@ int sg_amp_plan_create(int ndim, const double *W, int Lr, int Lc, int L, int M, 
                        sg_amp_plan **out);
 int sg_amp_plan_destroy(sg_amp_plan *p);
 int sg_amp_plan_info(const sg_amp_plan *p, int *w, int *nT, int *Mr, int *Mc, int *P, int *Q);
+/* Engine a decode of B codewords with this plan runs on: 0 general four-step
+ * (amp_dct.hip), 1 staged regular (amp_fused.hip), 2 per-codeword
+ * (amp_cw.hip), 3 block (amp_block.hip).  Reads SG_AMP_ENGINE like the
+ * decoder; returns the engine or a negative error code. */
+int sg_amp_plan_engine(const sg_amp_plan *p, int B);
 
 /* Batched AMP decode (sparc.py:883-999, one call per codeword in the
  * reference): y[B][n] received words sharing the plan's design; true_idx

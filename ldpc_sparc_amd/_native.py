@@ -68,6 +68,7 @@ SIGNATURES = [
                                       vp, vp, ct.c_int, ct.POINTER(vp)]),
     ("sg_amp_plan_destroy", ct.c_int, [vp]),
     ("sg_amp_plan_info", ct.c_int, [vp] + [ct.POINTER(ct.c_int)] * 6),
+    ("sg_amp_plan_engine", ct.c_int, [vp, ct.c_int]),
     ("sg_amp_decode", ct.c_int, [vp, vp, ct.c_int, vp, ct.c_double, ct.c_int, ct.c_double, ct.c_int,
                                  vp, vp, vp, vp]),
     ("sg_amp_decode_device", ct.c_int, [vp, vp, ct.c_int, vp, ct.c_double, ct.c_int, ct.c_double,
@@ -133,7 +134,7 @@ SG_INT_NAIVE, SG_INT_NAIVE_POST, SG_INT_DIFF, SG_INT_DIFF_POST = 0, 1, 2, 3
 INTEGRATED_MODES = {"naive": SG_INT_NAIVE, "naive_posteriors": SG_INT_NAIVE_POST, "integrated": SG_INT_DIFF,
                     "integrated_posteriors": SG_INT_DIFF_POST}
 
-SG_PH_COUNT = 8
+SG_PH_COUNT = 9
 
 
 def lib():

@@ -6,6 +6,7 @@
 #include <cmath>
 #include <complex>
 #include <memory>
+#include <type_traits>
 #include <vector>
 
 #include "amp.hpp"
@@ -52,6 +53,12 @@ struct sg_amp_plan {
     void *ws_s = nullptr, *ws_tu = nullptr, *ws_xn = nullptr, *ws_part = nullptr, *ws_stM = nullptr,
          *ws_stI = nullptr;
     double *ws_tau_prev = nullptr;
+    // per-codeword engine (amp_cw.hip), built beside the regular tables when eligible
+    bool cw = false;
+    int cwKT = 0;
+    uint32_t *c_kt = nullptr;
+    int32_t *c_oa = nullptr, *c_ob = nullptr, *c_gi = nullptr;
+    void *c_gc = nullptr;
     // block engine (several transforms per column block, amp_block.hip)
     bool block = false;
     uint16_t *b_gloc = nullptr;
@@ -175,7 +182,8 @@ static int ensure_ws(sg_amp_plan *p, int B, int t_max) {
     if (p->regular) {
         SG_ALLOC(p->ws_s, Bz * p->LM * rs);
         SG_ALLOC(p->ws_tu, Bz * p->nT * p->rQ * p->nRmax * 2 * rs);
-        SG_ALLOC(p->ws_xn, Bz * p->nT * p->nKmax * 2 * rs);
+        // (the per-codeword engine keeps its compact X here: KT * CW_THREADS per codeword)
+        SG_ALLOC(p->ws_xn, Bz * std::max(p->nT * p->nKmax, p->cwKT * CW_THREADS) * 2 * rs);
         SG_ALLOC(p->ws_part, Bz * p->nT * p->rQ * 3 * p->Lblk * rs);
         if (std::getenv("SG_AMP_TPROF")) {  // diagnostics only
             if (p->tprof) hipFree(p->tprof);
@@ -253,6 +261,71 @@ static AmpBufs<T> bufs(const sg_amp_plan *p, int B, const void *y) {
     return bf;
 }
 
+// Per-codeword engine tables (amp_cw.hip): the needed indices of each row go
+// to one thread (longest rows first, to the least loaded thread), so a thread
+// owns at most KT indices; compact index c = j * CW_THREADS + tid.
+static int build_cw(sg_amp_plan *p, const std::vector<int32_t> &row_k1, const std::vector<int32_t> &kptr,
+                    const std::vector<int32_t> &kk2, const std::vector<int32_t> &oa, const std::vector<int32_t> &ob,
+                    const std::vector<int32_t> &gi, const std::vector<cd> &gc) {
+    const int nr = (int)row_k1.size(), nk = kptr[nr], n = p->n;
+    std::vector<int> rows(nr);
+    for (int r = 0; r < nr; ++r) rows[r] = r;
+    std::stable_sort(rows.begin(), rows.end(),
+                     [&](int a, int b) { return kptr[a + 1] - kptr[a] > kptr[b + 1] - kptr[b]; });
+    std::vector<std::pair<int, int>> heap;  // (load, thread), min-heap
+    for (int i = 0; i < CW_THREADS; ++i) heap.push_back({0, i});
+    auto cmp = [](const std::pair<int, int> &a, const std::pair<int, int> &b) { return a > b; };
+    std::make_heap(heap.begin(), heap.end(), cmp);
+    std::vector<std::vector<int>> own(CW_THREADS);
+    int KT = 0;
+    for (int r : rows) {
+        std::pop_heap(heap.begin(), heap.end(), cmp);
+        auto &h = heap.back();
+        own[h.second].push_back(r);
+        h.first += kptr[r + 1] - kptr[r];
+        KT = std::max(KT, h.first);
+        std::push_heap(heap.begin(), heap.end(), cmp);
+    }
+    if (KT <= 24) KT = 24;
+    else if (KT <= 28) KT = 28;
+    else if (KT <= 32) KT = 32;
+    else return SG_OK;  // too many needed indices: the staged engine only
+    std::vector<uint32_t> kt((size_t)KT * CW_THREADS, 0u);
+    std::vector<int32_t> cmap(nk, -1);
+    for (int tid = 0; tid < CW_THREADS; ++tid) {
+        int j = 0;
+        for (int r : own[tid])
+            for (int k = kptr[r]; k < kptr[r + 1]; ++k, ++j) {
+                uint32_t e = (uint32_t)row_k1[r] | ((uint32_t)kk2[k] << 14) | CW_VALID;
+                if (k == kptr[r]) e |= CW_NEWROW;
+                if (k == kptr[r + 1] - 1) e |= CW_ENDROW;
+                kt[(size_t)j * CW_THREADS + tid] = e;
+                cmap[k] = j * CW_THREADS + tid;
+            }
+    }
+    // unused inverse terms: row 0 with coefficient 0 (the kernel reads all four)
+    std::vector<int32_t> c_oa(n), c_ob(n), c_gi((size_t)KT * CW_THREADS * 4, 0);
+    std::vector<cd> c_gc((size_t)KT * CW_THREADS * 4, cd(0, 0));
+    for (int i = 0; i < n; ++i) {
+        c_oa[i] = cmap[oa[i]];
+        c_ob[i] = cmap[ob[i]];
+    }
+    for (int k = 0; k < nk; ++k)
+        for (int q = 0; q < 4; ++q) {
+            const int32_t i = gi[(size_t)k * 4 + q];
+            c_gi[(size_t)cmap[k] * 4 + q] = i < 0 ? 0 : i;
+            c_gc[(size_t)cmap[k] * 4 + q] = i < 0 ? cd(0, 0) : gc[(size_t)k * 4 + q];
+        }
+    SG_TRY(upload(p, &p->c_kt, kt));
+    SG_TRY(upload(p, &p->c_oa, c_oa));
+    SG_TRY(upload(p, &p->c_ob, c_ob));
+    SG_TRY(upload(p, &p->c_gi, c_gi));
+    SG_TRY(upload_cx(p, &p->c_gc, c_gc));
+    p->cwKT = KT;
+    p->cw = true;
+    return SG_OK;
+}
+
 // Tables of the regular engine (amp_fused.hip), one transform per column
 // block: class order of each block's entries and the needed-row structure of
 // the two FFT stages.  Sizes: P = stage-1 FFT length (LDS resident), Q = N2/P.
@@ -264,7 +337,12 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
     SG_CHECK_ARG(Lblk < 65536, "too many sections per column block (%d)", Lblk);
     const size_t rb = p->precision == SG_F64 ? 8 : 4;
     long long Pmax = p->precision == SG_F64 ? 8192 : 16384;
-    if (const char *e = getenv("SG_AMP_PMAX")) Pmax = std::max(8LL, std::min(Pmax, atoll(e)));  // tuning knob
+    // SG_AMP_ENGINE=cw at plan creation: P = 8192 and the per-codeword engine's
+    // tables (single-precision single-transform designs; opt-in while it is
+    // slower than the staged engine at C2)
+    const char *eng = getenv("SG_AMP_ENGINE");
+    if (p->precision == SG_F32 && nT == 1 && eng && std::strcmp(eng, "cw") == 0) Pmax = 8192;
+    if (const char *e = getenv("SG_AMP_PMAX")) Pmax = std::max(8LL, std::min(16384LL, atoll(e)));  // tuning knob
     int P = (int)std::min<long long>(N2, Pmax);
     auto img_bound = [](int P) { return 2 * (P + (P >> 4)); };  // before the classes are known
     while (P > 8 && reg_stage1_lds(img_bound(P), P, Lblk, rb) > 160 * 1024) P >>= 1;
@@ -474,6 +552,9 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
     SG_TRY(upload_cx(p, &p->r_stw, stw));
     SG_TRY(upload_cx(p, &p->r_twa, twa));
     SG_TRY(upload_cx(p, &p->r_twb, twb));
+    if (p->precision == SG_F32 && nT == 1 && P == (1 << 13) && Lblk <= 2 * CW_THREADS &&
+        n <= 16 * CW_THREADS && Q <= 64 && p->rmaxcls <= (2 * P / CW_THREADS + 4) * CW_THREADS)
+        SG_TRY(build_cw(p, row_k1[0], kptr[0], kk2[0], f_oa, f_ob, f_gi, f_gc));
     return SG_OK;
 }
 
@@ -498,6 +579,30 @@ static RegTables<T> rtables(const sg_amp_plan *p) {
     const char *sk = std::getenv("SG_AMP_SKIP");  // timing ablation only: results are wrong when set
     tb.skip = sk ? std::atoi(sk) : 0;
     return tb;
+}
+
+static CwTables ctables(const sg_amp_plan *p) {
+    CwTables tb;
+    tb.L = p->L; tb.M = p->M; tb.LM = p->LM; tb.n = p->n; tb.Q = p->rQ; tb.Lblk = p->Lblk; tb.nB = p->nB;
+    tb.KT = p->cwKT; tb.log2P = p->rlog2P; tb.maxcls = p->rmaxcls;
+    tb.img = (std::max(p->rimg, p->n) + 3) / 4 * 4;  // FFT / class image, also z / phi
+    tb.kt = p->c_kt; tb.oa = p->c_oa; tb.ob = p->c_ob; tb.oc = (const cx<float> *)p->r_oc;
+    tb.gi = p->c_gi; tb.gc = (const cx<float> *)p->c_gc;
+    tb.cls_ptr = p->r_cls_ptr; tb.cls_ls = p->r_cls_ls; tb.qpos = p->r_qpos; tb.seg = p->r_seg;
+    tb.twQ = (const cx<float> *)p->r_twQ; tb.stw = (const cx<float> *)p->r_stw;
+    tb.twa = (const cx<float> *)p->r_twa; tb.twb = (const cx<float> *)p->r_twb;
+    tb.tprof = p->tprof;  // [B][32] stamps (the buffer holds B * Q * 20 >= 32 B words)
+    return tb;
+}
+
+// Engine choice for a decode of B codewords: the per-codeword engine keeps
+// one workgroup per codeword, so it wants a batch that fills the CUs.
+// SG_AMP_ENGINE=cw / staged forces either (tests, A/B).
+static bool use_cw(const sg_amp_plan *p, int B) {
+    if (!p->cw) return false;
+    const char *e = std::getenv("SG_AMP_ENGINE");
+    (void)B;
+    return e && std::strcmp(e, "cw") == 0;
 }
 
 template <typename T>
@@ -792,11 +897,17 @@ static int decode_regular(sg_amp_plan *p, const void *d_y, int B, const int32_t 
     pr.phi_method = phi_method; pr.t_max = t_max;
     SG_TRY(reg_launch_init(B, p->Lc, t_max, p->ws_nmse, p->ws_active, p->ws_tfinal, s));
     std::vector<int32_t> act(B);
+    const bool cw = std::is_same<T, float>::value && use_cw(p, B);
     for (int t = 0; t < t_max - 1; ++t) {
-        if (t > 0) SG_TRY(reg_launch_ab<T>(tb, bf, s));
-        SG_TRY(reg_launch_ctrl0<T>(tb, bf, sc, pr, t, s));
-        SG_TRY(reg_launch_az<T>(tb, bf, t, s));
-        SG_TRY(reg_launch_merge<T>(tb, bf, sc, pr, t, s));
+        if constexpr (std::is_same<T, float>::value) {
+            if (cw) SG_TRY(cw_launch_iter(ctables(p), bf, sc, pr, t, s));
+        }
+        if (!cw) {
+            if (t > 0) SG_TRY(reg_launch_ab<T>(tb, bf, s));
+            SG_TRY(reg_launch_ctrl0<T>(tb, bf, sc, pr, t, s));
+            SG_TRY(reg_launch_az<T>(tb, bf, t, s));
+            SG_TRY(reg_launch_merge<T>(tb, bf, sc, pr, t, s));
+        }
         if (t % 4 == 3 && t + 1 < t_max - 1 && !tb.skip) {  // skip the remaining launches once every codeword stopped
             SG_HIP(hipMemcpyAsync(act.data(), p->ws_active, sizeof(int32_t) * B, hipMemcpyDeviceToHost, s));
             SG_HIP(hipStreamSynchronize(s));
@@ -983,6 +1094,12 @@ int sg_amp_plan_destroy(sg_amp_plan *p) {
     if (p->tprof) hipFree(p->tprof);
     delete p;
     return SG_OK;
+}
+
+int sg_amp_plan_engine(const sg_amp_plan *p, int B) {
+    SG_CHECK_ARG(p, "plan is NULL");
+    if (p->regular) return (p->precision == SG_F32 && sg::use_cw(p, B)) ? 2 : 1;
+    return p->block ? 3 : 0;
 }
 
 int sg_amp_plan_info(const sg_amp_plan *p, int *w, int *nT, int *Mr, int *Mc, int *P, int *Q) {

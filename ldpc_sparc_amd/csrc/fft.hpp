@@ -253,6 +253,31 @@ __device__ __forceinline__ void tw_expand(const cx<T> *wl, cx<T> *w /* [R], w[0]
     }
 }
 
+// v[r] *= w^r with the products of tw_expand, each formed right before its
+// use (fewer live registers than the expanded w[R]; identical arithmetic)
+template <typename T, bool INV, int R>
+__device__ __forceinline__ void tw_apply(const cx<T> *wl, cx<T> *v) {
+    if constexpr (R == 16) {
+        cx<T> a[6];
+#pragma unroll
+        for (int t = 0; t < 6; ++t) a[t] = INV ? cconj(wl[t]) : wl[t];
+#pragma unroll
+        for (int b = 1; b < 4; ++b) v[b] = cmul(v[b], a[b - 1]);
+#pragma unroll
+        for (int q = 1; q < 4; ++q) {
+            const cx<T> wq = a[q + 2];  // w^4, w^8, w^12
+            v[4 * q] = cmul(v[4 * q], wq);
+#pragma unroll
+            for (int b = 1; b < 4; ++b) v[4 * q + b] = cmul(v[4 * q + b], cmul(wq, a[b - 1]));
+        }
+    } else {
+        cx<T> w[R];
+        tw_expand<T, INV, R>(wl, w);
+#pragma unroll
+        for (int r = 1; r < R; ++r) v[r] = cmul(v[r], w[r]);
+    }
+}
+
 template <typename T, bool INV, int R, int EPT>
 __device__ __forceinline__ void stockham1_stage(cx<T> *d, int log2n, int log2Ns, const cx<T> *__restrict__ stw,
                                                 int tid, int nthr) {
@@ -400,12 +425,7 @@ __device__ __forceinline__ void stockham1_stage_ct(cx<T> *d, const cx<T> *wl, in
         const int jp = fsw(j);
 #pragma unroll
         for (int r = 0; r < R; ++r) v[i * R + r] = d[(NBF % 256 == 0) ? jp + r * NBF : fsw(j + r * NBF)];
-        if constexpr (LOG2NS > 0) {
-            cx<T> w[R];
-            tw_expand<T, INV, R>(wl + i * tw_per_k(R), w);
-#pragma unroll
-            for (int r = 1; r < R; ++r) v[i * R + r] = cmul(v[i * R + r], w[r]);
-        }
+        if constexpr (LOG2NS > 0) tw_apply<T, INV, R>(wl + i * tw_per_k(R), &v[i * R]);
         dftR<T, INV, R>(&v[i * R]);
         base_out[i] = ((j - k) << LR) + k;
     }
@@ -439,6 +459,24 @@ __device__ __forceinline__ void lds_fft1_ct(cx<T> *d, const cx<T> *__restrict__ 
     cx<T> w0[N0 > 0 ? N0 : 1];
     fft1_tw_load_ct<T, EPT, LOG2N, 0>(stw, tid, w0);
     lds_fft1_ct_from<T, INV, EPT, LOG2N, 0>(d, stw, tid, w0);
+}
+
+// Variant without the next stage's twiddles in flight (fewer live registers
+// for kernels that hold other state across the FFT)
+template <typename T, bool INV, int EPT, int LOG2N, int ST>
+__device__ __forceinline__ void lds_fft1_ct_lean_from(cx<T> *d, const cx<T> *__restrict__ stw, int tid) {
+    if constexpr (ST < fft1_nstages_ct(LOG2N, EPT)) {
+        constexpr int R = fft1_radix_ct(LOG2N, EPT, ST);
+        constexpr int NW = fft1_twl_ct(LOG2N, EPT, ST);
+        cx<T> wl[NW > 0 ? NW : 1];
+        fft1_tw_load_ct<T, EPT, LOG2N, ST>(stw, tid, wl);
+        stockham1_stage_ct<T, INV, R, EPT, LOG2N, fft1_log2ns_ct(LOG2N, EPT, ST)>(d, wl, tid);
+        lds_fft1_ct_lean_from<T, INV, EPT, LOG2N, ST + 1>(d, stw, tid);
+    }
+}
+template <typename T, bool INV, int EPT, int LOG2N>
+__device__ __forceinline__ void lds_fft1_ct_lean(cx<T> *d, const cx<T> *__restrict__ stw, int tid) {
+    lds_fft1_ct_lean_from<T, INV, EPT, LOG2N, 0>(d, stw, tid);
 }
 
 }  // namespace sg

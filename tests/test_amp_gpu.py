@@ -260,3 +260,78 @@ def test_c4_block_engine_vs_general_engine(monkeypatch):
     assert np.mean(mb != mg) < 1e-3
     np.testing.assert_allclose(nb[:, :10], ng[:, :10], atol=1e-4)
     assert np.mean(mb != true) < 0.05  # the decode wave runs through at R = 1.5
+
+
+# ---- per-codeword engine (amp_cw.hip): opt-in with SG_AMP_ENGINE=cw (plan
+# creation builds its tables, decode runs it)
+
+@pytest.mark.parametrize("name,cp,dp,var,si", [c for c in all_seeds() if c[1].get('M') == 512 and
+                                              not c[1].get('power_allocated')])
+def test_cw_engine_f32_vs_reference(sparc_golden, monkeypatch, name, cp, dp, var, si):
+    """Regular designs with w >= 2^15 through the per-codeword engine, against
+    the reference's own outputs (the bar of test_decode_f32_tolerance)."""
+    key = f"{name}_s{si}"
+    W, L, M, n, o0, o1 = design(sparc_golden, name, si, cp, var)
+    if np.ndim(W) != 0:
+        pytest.skip("one transform per design only")
+    monkeypatch.setenv("SG_AMP_ENGINE", "cw")
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    dp = dict(dp)
+    sparc.check_decode_params(dp)
+    true = sparc.bin_arr_2_msg_vector(sparc_golden[key + "_bits"], M).reshape(L, M).argmax(1)
+    mi, tf, nmse, psi = sparc.amp_decode_batch(sparc_golden[key + "_y"][None], op, var, dp['t_max'],
+                                               dp['rtol'], dp['phi_est_method'], true[None],
+                                               precision=_native.SG_F32)
+    assert _native.lib().sg_amp_plan_engine(op.plan(_native.SG_F32), 1) == 2, "per-codeword engine not selected"
+    ref_map = sparc_golden[key + "_map"]
+    ref_nmse = sparc_golden[key + "_nmse"].reshape(nmse[0].shape)
+    if float(sparc_golden[key + "_sim_ber"]) == 0.0:
+        assert np.array_equal(mi[0], ref_map), key
+        assert abs(int(tf[0]) - int(sparc_golden[key + "_t_final"])) <= 2, key
+    np.testing.assert_allclose(nmse[0][:4], ref_nmse[:4], rtol=0, atol=1e-3, err_msg=key)
+
+
+def test_cw_engine_full_size_vs_staged_and_f64(monkeypatch):
+    """C2 geometry at R=1.3: the per-codeword engine decodes every codeword,
+    agrees with the staged engine on the decisions and tracks the f64 NMSE."""
+    W, L, M, n, o0, o1 = _c2_design(21, R=1.3)
+    rng = np.random.default_rng(9)
+    B = 6
+    true = rng.integers(0, M, (B, L))
+    beta0 = np.zeros((B, L * M))
+    beta0[np.arange(B)[:, None], np.arange(L) * M + true] = 1
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    Y = op.apply(beta0, False) + rng.standard_normal((B, n))
+    m64, t64, n64, _ = sparc.amp_decode_batch(Y, op, 1.0, 25, true_idx=true)
+    monkeypatch.setenv("SG_AMP_ENGINE", "cw")
+    mc, tc, nc, pc = sparc.amp_decode_batch(Y, op, 1.0, 25, true_idx=true, precision=_native.SG_F32)
+    assert _native.lib().sg_amp_plan_engine(op.plan(_native.SG_F32), B) == 2
+    monkeypatch.setenv("SG_AMP_ENGINE", "staged")
+    os_ = sparc.DesignOperator(W, L, M, n, o0, o1)  # staged tables (P = 16384)
+    ms, ts, ns, ps = sparc.amp_decode_batch(Y, os_, 1.0, 25, true_idx=true, precision=_native.SG_F32)
+    assert np.array_equal(mc, true) and np.array_equal(ms, true)
+    assert np.all(np.abs(tc - ts) <= 1) and np.all(np.abs(tc - t64) <= 2)
+    np.testing.assert_allclose(nc[:, :8], n64[:, :8], atol=2e-3)
+    np.testing.assert_allclose(nc[:, :8], ns[:, :8], atol=1e-4)
+
+
+def test_cw_engine_rate15_matches_staged(monkeypatch):
+    """C2 benchmark point (R=1.5, AMP does not decode): the two f32 engines
+    reach the same section decisions on almost every section and the same
+    iteration counts within one."""
+    W, L, M, n, o0, o1 = _c2_design(5)
+    rng = np.random.default_rng(12)
+    B = 3
+    true = rng.integers(0, M, (B, L))
+    beta0 = np.zeros((B, L * M))
+    beta0[np.arange(B)[:, None], np.arange(L) * M + true] = 1
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    Y = op.apply(beta0, False) + rng.standard_normal((B, n))
+    monkeypatch.setenv("SG_AMP_ENGINE", "cw")
+    mc, tc, nc, _ = sparc.amp_decode_batch(Y, op, 1.0, 25, true_idx=true, precision=_native.SG_F32)
+    monkeypatch.setenv("SG_AMP_ENGINE", "staged")
+    os_ = sparc.DesignOperator(W, L, M, n, o0, o1)
+    ms, ts, ns, _ = sparc.amp_decode_batch(Y, os_, 1.0, 25, true_idx=true, precision=_native.SG_F32)
+    assert np.mean(mc == ms) > 0.97
+    assert np.all(np.abs(tc - ts) <= 1)
+    np.testing.assert_allclose(nc[:, :6], ns[:, :6], atol=1e-3)
