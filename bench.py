@@ -482,9 +482,13 @@ def main():
     flops_per_cwit = 2 * 2.5 * w * np.log2(w) + 20 * st["L"] * st["M"]
     achieved = bytes_per_cwit * cw_it / (amp_ms * 1e-3) / 1e9 if amp_ms > 0 else None
     total_cw = d.world * st["B"] * args.steps
+    # the engine this batch ran on (2: per-codeword amp_cw.hip, 1: staged amp_fused.hip)
+    engine = _native.lib().sg_amp_plan_engine(st["plan"], st["B"])
+    engine_name = {1: "staged (amp_fused.hip)", 2: "per-codeword (amp_cw.hip)"}.get(engine, str(engine))
     traffic = None
-    tpath = os.path.join(REPO, "profiles", "r01_pmc_traffic_amp_c2.json")
-    if os.path.exists(tpath):  # rocprofv3 --pmc passes of tools/pmc_traffic.py (same kernels, B=64)
+    tfile = "r01_pmc_traffic_amp_c2_cw.json" if engine == 2 else "r01_pmc_traffic_amp_c2.json"
+    tpath = os.path.join(REPO, "profiles", tfile)
+    if os.path.exists(tpath):  # rocprofv3 --pmc passes of tools/pmc_traffic.py (same engine, B=256)
         with open(tpath) as f:
             traffic = json.load(f)["hbm_bytes_per_codeword_iteration"]
     out = {
@@ -510,8 +514,10 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                      "traffic_unit": "HBM bytes per codeword-iteration (PMC FETCH_SIZE*2 + WRITE_SIZE, "
-                                     "profiles/r01_pmc_traffic_amp_c2.json)",
-                     "kernel": "one AMP iteration = " + "+".join(AMP_PHASES),
+                                     f"profiles/{tfile})",
+                     "engine": engine_name,
+                     "kernel": ("cw_iter (one launch per AMP iteration)" if engine == 2 else
+                                "one AMP iteration = " + "+".join(AMP_PHASES[:6])),
                      "algorithmic_bytes_per_codeword_iteration": bytes_per_cwit,
                      "codeword_iterations": cw_it,
                      "kernel_ms": {k: round(v[0], 3) for k, v in phases.items()},

@@ -150,31 +150,32 @@ struct RegBufs {
 };
 
 // Per-codeword engine (amp_cw.hip): the regular design at the benchmark sizes
-// (single precision, one transform, P = 2^14, 512 threads), one workgroup per
+// (single precision, one transform, P = 2^13), one 1024-thread workgroup per
 // codeword running a whole AMP iteration -- every class of both transforms,
-// the residual and the section statistics -- without HBM intermediates.
-// The needed indices k = k1 + P k2 are owned by threads (all of a row's
-// indices by one thread), compact index c = j * 512 + tid, j < KT.  512
-// threads (two wavefronts per SIMD) leave 256 VGPRs per thread for the
-// accumulators beside the 32-element FFT.
-constexpr int CW_THREADS = 512;
+// the residual and the section statistics -- with the needed spectrum in LDS
+// and no HBM intermediates.  The needed indices k = k1 + P k2 are owned by
+// threads (all of a row's indices by one thread, at most KT per thread).
+constexpr int CW_THREADS = 1024;
+constexpr uint32_t CW_KMASK = (1u << 19) - 1;  // needed index k < N2 <= 2^19
 constexpr uint32_t CW_NEWROW = 1u << 20, CW_ENDROW = 1u << 21, CW_VALID = 1u << 22;
 struct CwTables {
-    int L, M, LM, n, Q, Lblk, nB, KT, log2P, maxcls;
+    int L, M, LM, n, N2, Q, Lblk, KT, log2P, maxcls;
+    int maxseg;               // longest section segment of a class
+    float inv_n2;             // 1 / N2
     int img;                  // LDS reals of the FFT / class image (>= z / phi)
-    const uint32_t *kt;       // [KT][512] k1 | k2 << 14 | flags
-    const int32_t *oa, *ob;   // [n] compact indices of the forward outputs' X[a], X[b]
+    const uint32_t *kt;       // [KT][1024] owned needed index k | flags; X / G slot j * 1024 + tid
+    const int32_t *oa, *ob;   // [n] slots of the forward outputs' X[a], X[b]
     const cx<float> *oc;      // [n][2]
-    const int32_t *gi;        // [KT * 512][4] inverse inputs (output row index or -1), compact order
-    const cx<float> *gc;      // [KT * 512][4]
+    const int32_t *gi;        // [KT * 1024][4] inverse inputs by slot (output row index; unused: 0)
+    const cx<float> *gc;      // [KT * 1024][4] (unused: 0)
     const int32_t *cls_ptr;   // [Q+1]
     const uint32_t *cls_ls;   // [Mc] padded real LDS index | section << 16
     const int32_t *qpos;      // [Mc]
     const uint16_t *seg;      // [Q][Lblk+1]
-    const cx<float> *twQ, *stw, *twa, *twb;
+    const cx<float> *stw;     // the P-point FFT's stage twiddles at 8 elements per thread
     uint64_t *tprof;          // diagnostics (SG_AMP_TPROF): [B][32] shader-clock stamps, or null
 };
-size_t cw_lds_bytes(int img, int KT, int Lblk, int nB, int Q);
+size_t cw_lds_bytes(int img, int nslots);
 int cw_launch_iter(const CwTables &tb, const RegBufs<float> &bf, const AmpScalars &sc, const AmpParams &pr, int t,
                    hipStream_t s);
 

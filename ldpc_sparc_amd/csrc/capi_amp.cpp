@@ -39,7 +39,7 @@ struct sg_amp_plan {
     int32_t *ws_active = nullptr, *ws_argmax = nullptr, *ws_true = nullptr, *ws_tfinal = nullptr;
     // regular engine (one transform per column block, amp_fused.hip)
     bool regular = false;
-    int rP = 0, rQ = 0, rlog2P = 0, rept = 0, rmaxcls = 0, rimg = 0, nRmax = 0, nKmax = 0, RB = 0, nrb = 0, maxKb = 0, Lblk = 0, nB = 0;
+    int rP = 0, rQ = 0, rlog2P = 0, rept = 0, rmaxcls = 0, rmaxseg = 0, rimg = 0, nRmax = 0, nKmax = 0, RB = 0, nrb = 0, maxKb = 0, Lblk = 0, nB = 0;
     uint32_t *r_row_k1p = nullptr;
     int32_t *r_nR = nullptr, *r_row_k1 = nullptr, *r_kptr = nullptr, *r_kk2 = nullptr, *r_krho = nullptr;
     int32_t *r_oa = nullptr, *r_ob = nullptr, *r_gi = nullptr, *r_cls_ptr = nullptr, *r_cls_j = nullptr,
@@ -58,7 +58,7 @@ struct sg_amp_plan {
     int cwKT = 0;
     uint32_t *c_kt = nullptr;
     int32_t *c_oa = nullptr, *c_ob = nullptr, *c_gi = nullptr;
-    void *c_gc = nullptr;
+    void *c_gc = nullptr, *c_stw = nullptr;
     // block engine (several transforms per column block, amp_block.hip)
     bool block = false;
     uint16_t *b_gloc = nullptr;
@@ -182,8 +182,7 @@ static int ensure_ws(sg_amp_plan *p, int B, int t_max) {
     if (p->regular) {
         SG_ALLOC(p->ws_s, Bz * p->LM * rs);
         SG_ALLOC(p->ws_tu, Bz * p->nT * p->rQ * p->nRmax * 2 * rs);
-        // (the per-codeword engine keeps its compact X here: KT * CW_THREADS per codeword)
-        SG_ALLOC(p->ws_xn, Bz * std::max(p->nT * p->nKmax, p->cwKT * CW_THREADS) * 2 * rs);
+        SG_ALLOC(p->ws_xn, Bz * p->nT * p->nKmax * 2 * rs);
         SG_ALLOC(p->ws_part, Bz * p->nT * p->rQ * 3 * p->Lblk * rs);
         if (std::getenv("SG_AMP_TPROF")) {  // diagnostics only
             if (p->tprof) hipFree(p->tprof);
@@ -263,11 +262,12 @@ static AmpBufs<T> bufs(const sg_amp_plan *p, int B, const void *y) {
 
 // Per-codeword engine tables (amp_cw.hip): the needed indices of each row go
 // to one thread (longest rows first, to the least loaded thread), so a thread
-// owns at most KT indices; compact index c = j * CW_THREADS + tid.
+// owns at most KT indices; slot (j, tid) at j * 1024 + tid.
 static int build_cw(sg_amp_plan *p, const std::vector<int32_t> &row_k1, const std::vector<int32_t> &kptr,
                     const std::vector<int32_t> &kk2, const std::vector<int32_t> &oa, const std::vector<int32_t> &ob,
                     const std::vector<int32_t> &gi, const std::vector<cd> &gc) {
-    const int nr = (int)row_k1.size(), nk = kptr[nr], n = p->n;
+    const int nr = (int)row_k1.size(), nk = kptr[nr];
+    if (nk > 12288) return SG_OK;  // X must fit LDS beside the 64 KB image
     std::vector<int> rows(nr);
     for (int r = 0; r < nr; ++r) rows[r] = r;
     std::stable_sort(rows.begin(), rows.end(),
@@ -286,24 +286,24 @@ static int build_cw(sg_amp_plan *p, const std::vector<int32_t> &row_k1, const st
         KT = std::max(KT, h.first);
         std::push_heap(heap.begin(), heap.end(), cmp);
     }
-    if (KT <= 24) KT = 24;
-    else if (KT <= 28) KT = 28;
-    else if (KT <= 32) KT = 32;
-    else return SG_OK;  // too many needed indices: the staged engine only
+    if (KT > 12) return SG_OK;  // X / G slots must fit LDS beside the image: the staged engine only
+    KT = 12;
+    const int P = p->rP, n = p->n;
     std::vector<uint32_t> kt((size_t)KT * CW_THREADS, 0u);
-    std::vector<int32_t> cmap(nk, -1);
+    std::vector<int32_t> cmap(nk, 0);
     for (int tid = 0; tid < CW_THREADS; ++tid) {
         int j = 0;
         for (int r : own[tid])
             for (int k = kptr[r]; k < kptr[r + 1]; ++k, ++j) {
-                uint32_t e = (uint32_t)row_k1[r] | ((uint32_t)kk2[k] << 14) | CW_VALID;
+                uint32_t e = ((uint32_t)row_k1[r] + (uint32_t)P * (uint32_t)kk2[k]) | CW_VALID;
                 if (k == kptr[r]) e |= CW_NEWROW;
                 if (k == kptr[r + 1] - 1) e |= CW_ENDROW;
                 kt[(size_t)j * CW_THREADS + tid] = e;
                 cmap[k] = j * CW_THREADS + tid;
             }
     }
-    // unused inverse terms: row 0 with coefficient 0 (the kernel reads all four)
+    // forward outputs and inverse terms by slot; unused inverse terms: row 0
+    // with coefficient 0 (the kernel reads all four)
     std::vector<int32_t> c_oa(n), c_ob(n), c_gi((size_t)KT * CW_THREADS * 4, 0);
     std::vector<cd> c_gc((size_t)KT * CW_THREADS * 4, cd(0, 0));
     for (int i = 0; i < n; ++i) {
@@ -313,14 +313,31 @@ static int build_cw(sg_amp_plan *p, const std::vector<int32_t> &row_k1, const st
     for (int k = 0; k < nk; ++k)
         for (int q = 0; q < 4; ++q) {
             const int32_t i = gi[(size_t)k * 4 + q];
-            c_gi[(size_t)cmap[k] * 4 + q] = i < 0 ? 0 : i;
-            c_gc[(size_t)cmap[k] * 4 + q] = i < 0 ? cd(0, 0) : gc[(size_t)k * 4 + q];
+            if (i >= 0) {
+                c_gi[(size_t)cmap[k] * 4 + q] = i;
+                c_gc[(size_t)cmap[k] * 4 + q] = gc[(size_t)k * 4 + q];
+            }
         }
+    // stage twiddles of the P-point FFT at 8 elements per thread (fft.hpp layout)
+    std::vector<cd> stw;
+    {
+        int radix[8];
+        const int ns = fft1_plan(p->rlog2P, 8, radix);
+        int lns = 0;
+        for (int st = 0; st < ns; ++st) {
+            const int R = radix[st];
+            const long long Ns = 1LL << lns;
+            for (long long k = 0; k < Ns; ++k)
+                for (int q = 0; q < tw_per_k(R); ++q) stw.push_back(tw(tw_exp(R, q) * k, Ns * R));
+            lns += ilog2(R);
+        }
+    }
     SG_TRY(upload(p, &p->c_kt, kt));
     SG_TRY(upload(p, &p->c_oa, c_oa));
     SG_TRY(upload(p, &p->c_ob, c_ob));
     SG_TRY(upload(p, &p->c_gi, c_gi));
     SG_TRY(upload_cx(p, &p->c_gc, c_gc));
+    SG_TRY(upload_cx(p, &p->c_stw, stw));
     p->cwKT = KT;
     p->cw = true;
     return SG_OK;
@@ -337,11 +354,13 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
     SG_CHECK_ARG(Lblk < 65536, "too many sections per column block (%d)", Lblk);
     const size_t rb = p->precision == SG_F64 ? 8 : 4;
     long long Pmax = p->precision == SG_F64 ? 8192 : 16384;
-    // SG_AMP_ENGINE=cw at plan creation: P = 8192 and the per-codeword engine's
-    // tables (single-precision single-transform designs; opt-in while it is
-    // slower than the staged engine at C2)
+    // Single-precision single-transform designs whose needed spectrum fits the
+    // per-codeword engine's LDS (2 n <= 12288 indices, L <= 1024): P = 8192 and
+    // its tables; SG_AMP_ENGINE=staged at plan creation keeps P = 16384
     const char *eng = getenv("SG_AMP_ENGINE");
-    if (p->precision == SG_F32 && nT == 1 && eng && std::strcmp(eng, "cw") == 0) Pmax = 8192;
+    if (p->precision == SG_F32 && nT == 1 && 2 * n <= 12 * CW_THREADS && Lblk <= CW_THREADS && N2 >= (1 << 14) &&
+        !(eng && std::strcmp(eng, "staged") == 0))
+        Pmax = 8192;
     if (const char *e = getenv("SG_AMP_PMAX")) Pmax = std::max(8LL, std::min(16384LL, atoll(e)));  // tuning knob
     int P = (int)std::min<long long>(N2, Pmax);
     auto img_bound = [](int P) { return 2 * (P + (P >> 4)); };  // before the classes are known
@@ -396,6 +415,7 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
             for (int l = 0; l <= Lblk; ++l) {
                 while (q < q1 && cls_sec[(size_t)t * Mc + q] < l) ++q;
                 sg[l] = (uint16_t)(q - q0);
+                if (l > 0) p->rmaxseg = std::max(p->rmaxseg, (int)sg[l] - (int)sg[l - 1]);
             }
         }
         // ---- needed N/2-indices: forward outputs = inverse inputs
@@ -552,8 +572,8 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
     SG_TRY(upload_cx(p, &p->r_stw, stw));
     SG_TRY(upload_cx(p, &p->r_twa, twa));
     SG_TRY(upload_cx(p, &p->r_twb, twb));
-    if (p->precision == SG_F32 && nT == 1 && P == (1 << 13) && Lblk <= 2 * CW_THREADS &&
-        n <= 16 * CW_THREADS && Q <= 64 && p->rmaxcls <= (2 * P / CW_THREADS + 4) * CW_THREADS)
+    if (p->precision == SG_F32 && nT == 1 && P == (1 << 13) && Lblk <= CW_THREADS && n <= 8 * CW_THREADS &&
+        Q <= 64 && p->rmaxcls <= 10 * CW_THREADS && p->rimg == 2 * P && fpad(p->rmaxcls + 16) < p->rimg)
         SG_TRY(build_cw(p, row_k1[0], kptr[0], kk2[0], f_oa, f_ob, f_gi, f_gc));
     return SG_OK;
 }
@@ -583,26 +603,27 @@ static RegTables<T> rtables(const sg_amp_plan *p) {
 
 static CwTables ctables(const sg_amp_plan *p) {
     CwTables tb;
-    tb.L = p->L; tb.M = p->M; tb.LM = p->LM; tb.n = p->n; tb.Q = p->rQ; tb.Lblk = p->Lblk; tb.nB = p->nB;
-    tb.KT = p->cwKT; tb.log2P = p->rlog2P; tb.maxcls = p->rmaxcls;
-    tb.img = (std::max(p->rimg, p->n) + 3) / 4 * 4;  // FFT / class image, also z / phi
+    tb.L = p->L; tb.M = p->M; tb.LM = p->LM; tb.n = p->n; tb.N2 = p->N2; tb.Q = p->rQ; tb.Lblk = p->Lblk;
+    tb.KT = p->cwKT; tb.log2P = p->rlog2P; tb.maxcls = p->rmaxcls; tb.maxseg = p->rmaxseg;
+    tb.img = p->rimg;
     tb.kt = p->c_kt; tb.oa = p->c_oa; tb.ob = p->c_ob; tb.oc = (const cx<float> *)p->r_oc;
     tb.gi = p->c_gi; tb.gc = (const cx<float> *)p->c_gc;
     tb.cls_ptr = p->r_cls_ptr; tb.cls_ls = p->r_cls_ls; tb.qpos = p->r_qpos; tb.seg = p->r_seg;
-    tb.twQ = (const cx<float> *)p->r_twQ; tb.stw = (const cx<float> *)p->r_stw;
-    tb.twa = (const cx<float> *)p->r_twa; tb.twb = (const cx<float> *)p->r_twb;
+    tb.stw = (const cx<float> *)p->c_stw;
+    tb.inv_n2 = 1.0f / (float)p->N2;
     tb.tprof = p->tprof;  // [B][32] stamps (the buffer holds B * Q * 20 >= 32 B words)
     return tb;
 }
 
 // Engine choice for a decode of B codewords: the per-codeword engine keeps
 // one workgroup per codeword, so it wants a batch that fills the CUs.
-// SG_AMP_ENGINE=cw / staged forces either (tests, A/B).
+// SG_AMP_ENGINE=cw / staged forces either at decode time (tests, A/B).
 static bool use_cw(const sg_amp_plan *p, int B) {
     if (!p->cw) return false;
     const char *e = std::getenv("SG_AMP_ENGINE");
-    (void)B;
-    return e && std::strcmp(e, "cw") == 0;
+    if (e && std::strcmp(e, "cw") == 0) return true;
+    if (e && std::strcmp(e, "staged") == 0) return false;
+    return B >= device_cu_count() / 2;
 }
 
 template <typename T>

@@ -144,10 +144,10 @@ def test_standalone_estimators():
     assert np.array_equal(sparc.msg_vector_map_estimator(s, 32), sparc_ref.map_estimator(s, 32))
 
 
-def _c2_design(seed, R=1.5):
+def _c2_design(seed, R=1.5, P=15.0):
     L, M = 1024, 512
     n = int(round(L * 9 / R))
-    W = np.array(15.0)
+    W = np.array(P)
     o0, o1 = sparc.generate_ordering(W, n, L * M, seed)
     return W, L, M, n, o0, o1
 
@@ -291,10 +291,16 @@ def test_cw_engine_f32_vs_reference(sparc_golden, monkeypatch, name, cp, dp, var
     np.testing.assert_allclose(nmse[0][:4], ref_nmse[:4], rtol=0, atol=1e-3, err_msg=key)
 
 
-def test_cw_engine_full_size_vs_staged_and_f64(monkeypatch):
-    """C2 geometry at R=1.3: the per-codeword engine decodes every codeword,
-    agrees with the staged engine on the decisions and tracks the f64 NMSE."""
-    W, L, M, n, o0, o1 = _c2_design(21, R=1.3)
+@pytest.mark.parametrize("L,R,P", [(512, 1.2, 15.0)])
+def test_cw_engine_full_size_vs_staged_and_f64(monkeypatch, L, R, P):
+    """A w=2^19 design where AMP decodes (L=512, M=512, R=1.2; with flat power
+    the n=6144 C2 geometry does not decode at any P, see the R=1.5 test
+    below): the per-codeword engine decodes every codeword, agrees with the
+    staged engine on the decisions and tracks the f64 NMSE."""
+    M = 512
+    n = int(round(L * 9 / R))
+    W = np.array(P)
+    o0, o1 = sparc.generate_ordering(W, n, L * M, 21)
     rng = np.random.default_rng(9)
     B = 6
     true = rng.integers(0, M, (B, L))

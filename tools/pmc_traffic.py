@@ -9,7 +9,7 @@ import csv
 import json
 import sys
 
-AMP = ("reg_ab_stage1", "reg_ab_stage2", "reg_az_stage1", "reg_az_stage2", "reg_merge", "reg_ctrl0")
+AMP = ("reg_ab_stage1", "reg_ab_stage2", "reg_az_stage1", "reg_az_stage2", "reg_merge", "reg_ctrl0", "cw_iter")
 
 
 def load(path, counter):
