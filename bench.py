@@ -140,6 +140,17 @@ class HostCounterComm:
         pass
 
 
+def pmc_traffic(section, field):
+    """HBM bytes per unit from the committed PMC passes of tools/pmc_bench.sh
+    (profiles/r01_pmc_traffic_bench.json), or None."""
+    path = os.path.join(REPO, "profiles", "r01_pmc_traffic_bench.json")
+    try:
+        with open(path) as f:
+            return json.load(f)[section][field]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 # ------------------------------------------------------------------ AMP (C2)
 
 def amp_setup(args, rank, rate=None):
@@ -376,7 +387,10 @@ def sc_bench(args, d, comm, cpu_seconds):
            "avg_iterations": float(tf.mean()), "section_errors": int(cnt[0]), "codeword_errors": int(cnt[2]),
            "ser": float(cnt[0]) / (d.world * B * L),
            "roofline": {"bound": "valu-f32", "achieved": ach, "peak": VALU_PEAK_TFS, "unit": "TFLOP/s",
-                        "frac": ach / VALU_PEAK_TFS if ach else None, "traffic": None,
+                        "frac": ach / VALU_PEAK_TFS if ach else None,
+                        "traffic": pmc_traffic("sc", "hbm_bytes_per_codeword_iteration_approx"),
+                        "traffic_unit": "HBM bytes per codeword-iteration, block-engine kernels (PMC, "
+                                        "profiles/r01_pmc_traffic_bench.json)",
                         "kernel": "blk_ab + blk_g + blk_az + control (amp_block.hip)",
                         "algorithmic_flops_per_codeword_iteration": flops,
                         "note": "2 nT transforms x 2.5 w log2 w + 20 L M per codeword-iteration; each transform "
@@ -576,7 +590,10 @@ def main():
                      "batch_per_gpu": bst["B"], "avg_executed_iterations": float(exec_it.mean()),
                      "frame_errors": int(bcnt[1]), "bit_errors": int(bcnt[0]),
                      "roofline": {"bound": "hbm", "achieved": bach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                  "frac": bach / HBM_PEAK_GBS if bach else None, "traffic": None,
+                                  "frac": bach / HBM_PEAK_GBS if bach else None,
+                                  "traffic": pmc_traffic("bp", "hbm_bytes_per_codeword_iteration"),
+                                  "traffic_unit": "HBM bytes per codeword-iteration (PMC, messages stay in LDS; "
+                                                  "profiles/r01_pmc_traffic_bench.json)",
                                   "kernel": "bp_flood_kernel<float, minsum>",
                                   "algorithmic_bytes_per_codeword_iteration": bbytes,
                                   "kernel_ms": bp_ms, "launches": ph.get("bp_flood", (0, 0))[1]}}
