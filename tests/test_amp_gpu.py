@@ -341,3 +341,27 @@ def test_cw_engine_rate15_matches_staged(monkeypatch):
     assert np.mean(mc == ms) > 0.97
     assert np.all(np.abs(tc - ts) <= 1)
     np.testing.assert_allclose(nc[:, :6], ns[:, :6], atol=1e-3)
+
+
+@pytest.mark.parametrize("phi_method", [1, 2])
+def test_cw_engine_phi_methods_match_staged(monkeypatch, phi_method):
+    """Both phi estimates (sparc.py:949-955) through the per-codeword engine
+    agree with the staged engine on an L=32, M=512 design (w = 2^15)."""
+    L, M, R = 32, 512, 1.3
+    n = int(round(L * 9 / R))
+    W = np.array(15.0)
+    o0, o1 = sparc.generate_ordering(W, n, L * M, 17)
+    rng = np.random.default_rng(3)
+    B = 5
+    true = rng.integers(0, M, (B, L))
+    beta0 = np.zeros((B, L * M))
+    beta0[np.arange(B)[:, None], np.arange(L) * M + true] = 1
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    Y = op.apply(beta0, False) + rng.standard_normal((B, n))
+    m64, t64, n64, _ = sparc.amp_decode_batch(Y, op, 1.0, 25, 1e-6, phi_method, true)
+    monkeypatch.setenv("SG_AMP_ENGINE", "cw")
+    mc, tc, nc, _ = sparc.amp_decode_batch(Y, op, 1.0, 25, 1e-6, phi_method, true, precision=_native.SG_F32)
+    assert _native.lib().sg_amp_plan_engine(op.plan(_native.SG_F32), B) == 2
+    assert np.array_equal(mc, m64)
+    assert np.all(np.abs(tc - t64) <= 2)
+    np.testing.assert_allclose(nc[:, :6], n64[:, :6], atol=1e-3)
