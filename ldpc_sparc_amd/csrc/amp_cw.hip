@@ -59,13 +59,30 @@ __device__ __forceinline__ cx<float> cw_w(const CwTables &tb, uint32_t j) {
     return {__builtin_amdgcn_cosf(x), -__builtin_amdgcn_sinf(x)};
 }
 
+// Radix plan of the P-point FFT at 8 values per thread (CW_RADIX_PLAN 0:
+// fft.hpp's 4, 4, 8, 8, 8; 1: 8, 8, 8, 8, 2; 2: 2, 8, 8, 8, 8)
+#ifndef CW_RADIX_PLAN
+#define CW_RADIX_PLAN 1
+#endif
+constexpr int cw_nstages() { return 5; }
+constexpr int cw_radix(int st) {
+    return CW_RADIX_PLAN == 0 ? fft1_radix_ct(CW_LOG2P, CW_EPT, st)
+           : CW_RADIX_PLAN == 1 ? (st < 4 ? 8 : 2)
+                                : (st == 0 ? 2 : 8);
+}
+constexpr int cw_log2ns(int st) {
+    int l = 0;
+    for (int i = 0; i < st; ++i) l += cw_radix(i) == 2 ? 1 : cw_radix(i) == 4 ? 2 : 3;
+    return l;
+}
+
 // The P-point LDS FFT (fft.hpp stages) with its stage twiddles
 // w_{Ns R}^(e k) from the hardware sine / cosine instead of a table: no
 // global loads between its barriers.
 template <bool INV, int ST>
 __device__ __forceinline__ void cw_fft_from(cx<float> *d, int tid) {
-    if constexpr (ST < fft1_nstages_ct(CW_LOG2P, CW_EPT)) {
-        constexpr int R = fft1_radix_ct(CW_LOG2P, CW_EPT, ST), LNS = fft1_log2ns_ct(CW_LOG2P, CW_EPT, ST);
+    if constexpr (ST < cw_nstages()) {
+        constexpr int R = cw_radix(ST), LNS = cw_log2ns(ST);
         constexpr int NB = CW_EPT / R, TWN = tw_per_k(R);
         cx<float> wl[LNS > 0 ? NB * TWN : 1];
         if constexpr (LNS > 0) {
