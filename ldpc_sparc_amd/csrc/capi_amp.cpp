@@ -623,7 +623,12 @@ static bool use_cw(const sg_amp_plan *p, int B) {
     const char *e = std::getenv("SG_AMP_ENGINE");
     if (e && std::strcmp(e, "cw") == 0) return true;
     if (e && std::strcmp(e, "staged") == 0) return false;
-    return B >= device_cu_count() / 2;
+    // one workgroup per codeword and CU: worth it when the batch fills whole
+    // waves of the CUs (at B = CUs it is ~11 % ahead of the staged engine,
+    // which keeps every CU busy at any B)
+    const int cu = std::max(device_cu_count(), 1);
+    const int waves = (B + cu - 1) / cu;
+    return B >= cu && (double)B / ((double)waves * cu) >= 0.9;
 }
 
 template <typename T>
