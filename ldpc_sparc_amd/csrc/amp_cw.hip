@@ -19,7 +19,8 @@
 //   merge section max and 1/sum, psi, NMSE, early stop (sparc.py:973-988)
 // LDS: the P-point image (64 KB) and X/G (12 x 1024 slots, 96 KB) -- all of it.
 // The class slice of s and its table entries for class m2 + 1 are in flight
-// in registers under class m2's FFT (Ab) or statistics (Az).  HBM traffic per
+// in registers under class m2's accumulation (Ab) or store and statistics
+// (Az); every twiddle comes from the hardware sine / cosine.  HBM traffic per
 // codeword-iteration is s read twice and written once (3 * 4 LM bytes) plus
 // z, y and the tables shared by every codeword (L2-resident).
 #include "amp.hpp"
