@@ -49,6 +49,7 @@ __device__ __forceinline__ double cw_block_sum(double v, double *red) {
 constexpr int CW_LOG2P = 13, CW_P = 1 << CW_LOG2P, CW_EPT = CW_P / CW_THREADS;
 constexpr int CW_SN = 10;  // class entries per thread (host: largest class <= CW_SN * 1024)
 constexpr int CW_CO = 8;   // output rows per thread (host: n <= CW_CO * 1024)
+constexpr int CW_KL = 12;  // X / G slots per thread in LDS (96 KB); any further ones in registers
 
 // w_N2^j = exp(-2 pi i j / N2) from the hardware sine / cosine, whose
 // argument is in revolutions: j mod N2 scaled by 1/N2 is exact in f32
@@ -130,11 +131,14 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
     const float inv_tp = have_beta ? (float)(1.0 / bf.tau[cw]) : 1.f;
     float *s = bf.s + (size_t)cw * tb.LM;
     // owned needed indices k | flags, slot j * 1024 + tid of X / G
+    constexpr int KR = KT > CW_KL ? KT - CW_KL : 1;  // register-held slots (j >= CW_KL)
     uint32_t kt[KT];
+    cx<float> Xr[KR];
 #pragma unroll
     for (int j = 0; j < KT; ++j) {
         kt[j] = tb.kt[j * CW_THREADS + tid];
-        Xl[j * CW_THREADS + tid] = {0.f, 0.f};
+        if (j < CW_KL) Xl[j * CW_THREADS + tid] = {0.f, 0.f};
+        else Xr[j - CW_KL] = {0.f, 0.f};
     }
     CW_TP(0);
 
@@ -188,10 +192,11 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
 #pragma unroll
                 for (int j = 0; j < KT; ++j) {  // invalid slots accumulate into themselves, unused
                     const cx<float> Tv = d[fsw(kt[j] & (CW_P - 1))];
-                    cx<float> x = Xl[j * CW_THREADS + tl];
+                    cx<float> x = j < CW_KL ? Xl[j * CW_THREADS + tl] : Xr[j < CW_KL ? 0 : j - CW_KL];
                     x.x += Tv.x * w[j].x - Tv.y * w[j].y;
                     x.y += Tv.x * w[j].y + Tv.y * w[j].x;
-                    Xl[j * CW_THREADS + tl] = x;
+                    if (j < CW_KL) Xl[j * CW_THREADS + tl] = x;
+                    else Xr[j < CW_KL ? 0 : j - CW_KL] = x;
                 }
             }
             __syncthreads();
@@ -218,6 +223,12 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
             sc.bcoef[cw] = g / ph;
         }
         bco = (float)(g / ph);
+        if constexpr (KT > CW_KL) {  // the register-held slots into the (free) image for the residual
+            __syncthreads();
+#pragma unroll
+            for (int j = CW_KL; j < KT; ++j) d[(j - CW_KL) * CW_THREADS + tid] = Xr[j - CW_KL];
+            __syncthreads();
+        }
     } else {
         g = pr.W[0];
         if (tid == 0) sc.gamma[cw] = g;
@@ -244,7 +255,8 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
         for (int k = 0; k < CW_CO; ++k) {
             float zn = yv[k];
             if (have_beta) {  // Onsager residual, sparc.py:943-946
-                const cx<float> ha = Xl[ia[k]], hb = Xl[ib[k]];
+                const cx<float> ha = ia[k] < CW_KL * CW_THREADS ? Xl[ia[k]] : d[ia[k] - CW_KL * CW_THREADS];
+                const cx<float> hb = ib[k] < CW_KL * CW_THREADS ? Xl[ib[k]] : d[ib[k] - CW_KL * CW_THREADS];
                 float r = 0.f;
                 r += (c1[k].x * ha.x - c1[k].y * ha.y) + (c2[k].x * hb.x + c2[k].y * hb.y);
                 zn = (yv[k] - r) + bco * zv[k];
@@ -274,14 +286,16 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
     }
     const float tau = (float)tv_new, inv_tau = (float)(1.0 / tv_new);
     const float phf = (float)phi;
-    float *zl = dr;  // z / phi, sparc.py:972
+    float *zl = dr + (KT > CW_KL ? 2 * (KT - CW_KL) * CW_THREADS : 0);  // z / phi (sparc.py:972), after those slots
 #pragma unroll
     for (int k = 0; k < CW_CO; ++k) {
         const int i = tid + k * CW_THREADS;
         if (i < tb.n) zl[i] = zr[k] / phf;
     }
     __syncthreads();
-    for (int c = tid; c < KT * CW_THREADS; c += CW_THREADS) {  // G by slot (unused terms: index 0, coefficient 0)
+#pragma unroll
+    for (int j = 0; j < KT; ++j) {  // G by slot (unused terms: index 0, coefficient 0)
+        const int c = j * CW_THREADS + tid;
         const int4 gi = reinterpret_cast<const int4 *>(tb.gi)[c];
         const float4 ga = reinterpret_cast<const float4 *>(tb.gc)[2 * c];
         const float4 gb = reinterpret_cast<const float4 *>(tb.gc)[2 * c + 1];
@@ -298,7 +312,8 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
         v = zl[gi.w];
         a.x += gb.z * v;
         a.y += gb.w * v;
-        Xl[c] = a;
+        if (j < CW_KL) Xl[c] = a;
+        else Xr[j < CW_KL ? 0 : j - CW_KL] = a;
     }
     __syncthreads();
     CW_TP(2);
@@ -334,7 +349,7 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
 #pragma unroll
             for (int j = 0; j < KT; ++j) {
                 if (!(kt[j] & CW_VALID)) continue;
-                const cx<float> gv = Xl[j * CW_THREADS + tl];
+                const cx<float> gv = j < CW_KL ? Xl[j * CW_THREADS + tl] : Xr[j < CW_KL ? 0 : j - CW_KL];
                 if (kt[j] & CW_NEWROW) u = {0.f, 0.f};
                 u.x += gv.x * w[j].x + gv.y * w[j].y;  // G conj(w_N2^(m2 k))
                 u.y += gv.y * w[j].x - gv.x * w[j].y;
@@ -475,7 +490,7 @@ static int cw_launch(const CwTables &tb, const RegBufs<float> &bf, const AmpScal
         SG_HIP(hipFuncSetAttribute((const void *)cw_iter<KT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr = true;
     }
-    const size_t lds = cw_lds_bytes(tb.img, KT * CW_THREADS);
+    const size_t lds = cw_lds_bytes(tb.img, CW_KL * CW_THREADS);
     if (lds > 160 * 1024) return fail(SG_ERR_UNSUPPORTED, "per-codeword engine: %zu bytes of LDS", lds);
     hipLaunchKernelGGL((cw_iter<KT>), dim3(bf.B), dim3(CW_THREADS), lds, s, tb, bf, sc, pr, t);
     return SG_OK;
@@ -488,8 +503,9 @@ int cw_launch_iter(const CwTables &tb, const RegBufs<float> &bf, const AmpScalar
         tb.maxcls > CW_SN * CW_THREADS || tb.img < 2 * CW_P || fpad(tb.maxcls + 16) >= tb.img)
         return fail(SG_ERR_UNSUPPORTED, "per-codeword engine: sizes outside its compile-time bounds");
     ProfScope ps(SG_PH_AMP_CW, s);
-    if (tb.KT != 12) return fail(SG_ERR_UNSUPPORTED, "per-codeword engine: %d indices per thread", tb.KT);
-    SG_TRY(cw_launch<12>(tb, bf, sc, pr, t, s));
+    if (tb.KT == 12) SG_TRY(cw_launch<12>(tb, bf, sc, pr, t, s));
+    else if (tb.KT == 14) SG_TRY(cw_launch<14>(tb, bf, sc, pr, t, s));
+    else return fail(SG_ERR_UNSUPPORTED, "per-codeword engine: %d indices per thread", tb.KT);
     SG_HIP(hipGetLastError());
     return SG_OK;
 }

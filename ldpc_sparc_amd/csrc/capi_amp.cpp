@@ -267,7 +267,7 @@ static int build_cw(sg_amp_plan *p, const std::vector<int32_t> &row_k1, const st
                     const std::vector<int32_t> &kk2, const std::vector<int32_t> &oa, const std::vector<int32_t> &ob,
                     const std::vector<int32_t> &gi, const std::vector<cd> &gc) {
     const int nr = (int)row_k1.size(), nk = kptr[nr];
-    if (nk > 12288) return SG_OK;  // X must fit LDS beside the 64 KB image
+    if (nk > 14 * CW_THREADS) return SG_OK;  // 12 slots per thread in LDS beside the image, 2 in registers
     std::vector<int> rows(nr);
     for (int r = 0; r < nr; ++r) rows[r] = r;
     std::stable_sort(rows.begin(), rows.end(),
@@ -286,8 +286,8 @@ static int build_cw(sg_amp_plan *p, const std::vector<int32_t> &row_k1, const st
         KT = std::max(KT, h.first);
         std::push_heap(heap.begin(), heap.end(), cmp);
     }
-    if (KT > 12) return SG_OK;  // X / G slots must fit LDS beside the image: the staged engine only
-    KT = 12;
+    if (KT > 14) return SG_OK;  // the staged engine only
+    KT = KT <= 12 ? 12 : 14;   // kernel instances (cw_iter<12>: all slots in LDS; <14>: two in registers)
     const int P = p->rP, n = p->n;
     std::vector<uint32_t> kt((size_t)KT * CW_THREADS, 0u);
     std::vector<int32_t> cmap(nk, 0);
@@ -358,7 +358,7 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
     // per-codeword engine's LDS (2 n <= 12288 indices, L <= 1024): P = 8192 and
     // its tables; SG_AMP_ENGINE=staged at plan creation keeps P = 16384
     const char *eng = getenv("SG_AMP_ENGINE");
-    if (p->precision == SG_F32 && nT == 1 && 2 * n <= 12 * CW_THREADS && Lblk <= CW_THREADS && N2 >= (1 << 14) &&
+    if (p->precision == SG_F32 && nT == 1 && 2 * n <= 14 * CW_THREADS && Lblk <= CW_THREADS && N2 >= (1 << 14) &&
         !(eng && std::strcmp(eng, "staged") == 0))
         Pmax = 8192;
     if (const char *e = getenv("SG_AMP_PMAX")) Pmax = std::max(8LL, std::min(16384LL, atoll(e)));  // tuning knob
@@ -923,7 +923,9 @@ static int decode_regular(sg_amp_plan *p, const void *d_y, int B, const int32_t 
     pr.phi_method = phi_method; pr.t_max = t_max;
     SG_TRY(reg_launch_init(B, p->Lc, t_max, p->ws_nmse, p->ws_active, p->ws_tfinal, s));
     std::vector<int32_t> act(B);
-    const bool cw = std::is_same<T, float>::value && use_cw(p, B);
+    bool cw = std::is_same<T, float>::value && use_cw(p, B);
+    const char *eng = std::getenv("SG_AMP_ENGINE");
+    const bool cw_forced = eng && std::strcmp(eng, "cw") == 0;
     for (int t = 0; t < t_max - 1; ++t) {
         if constexpr (std::is_same<T, float>::value) {
             if (cw) SG_TRY(cw_launch_iter(ctables(p), bf, sc, pr, t, s));
@@ -934,12 +936,21 @@ static int decode_regular(sg_amp_plan *p, const void *d_y, int B, const int32_t 
             SG_TRY(reg_launch_az<T>(tb, bf, t, s));
             SG_TRY(reg_launch_merge<T>(tb, bf, sc, pr, t, s));
         }
-        if (t % 4 == 3 && t + 1 < t_max - 1 && !tb.skip) {  // skip the remaining launches once every codeword stopped
+        // Poll the active flags: stop once every codeword has stopped, and
+        // hand the remaining iterations to the staged engine once half of the
+        // batch has stopped -- the per-codeword engine keeps one CU per
+        // codeword, so stopped codewords leave CUs idle, while the staged
+        // engine spreads the active ones over every CU.  Both keep the same
+        // state (s in class order, section statistics, scalars), so the
+        // switch is seamless.
+        const bool poll = cw && !cw_forced ? (t % 2 == 1) : (t % 4 == 3);
+        if (poll && t + 1 < t_max - 1 && !tb.skip) {
             SG_HIP(hipMemcpyAsync(act.data(), p->ws_active, sizeof(int32_t) * B, hipMemcpyDeviceToHost, s));
             SG_HIP(hipStreamSynchronize(s));
-            bool any = false;
-            for (int b = 0; b < B; ++b) any |= act[b] != 0;
-            if (!any) break;
+            int na = 0;
+            for (int b = 0; b < B; ++b) na += act[b] != 0;
+            if (na == 0) break;
+            if (cw && !cw_forced && 2 * na < B) cw = false;
         }
     }
     SG_HIP(hipMemsetAsync(p->ws_argmax, 0x7f, sizeof(int32_t) * B * p->L, s));

@@ -291,12 +291,13 @@ def test_cw_engine_f32_vs_reference(sparc_golden, monkeypatch, name, cp, dp, var
     np.testing.assert_allclose(nmse[0][:4], ref_nmse[:4], rtol=0, atol=1e-3, err_msg=key)
 
 
-@pytest.mark.parametrize("L,R,P", [(512, 1.2, 15.0)])
+@pytest.mark.parametrize("L,R,P", [(512, 1.2, 15.0), (1024, 1.3, 15.0)])
 def test_cw_engine_full_size_vs_staged_and_f64(monkeypatch, L, R, P):
-    """A w=2^19 design where AMP decodes (L=512, M=512, R=1.2; with flat power
-    the n=6144 C2 geometry does not decode at any P, see the R=1.5 test
-    below): the per-codeword engine decodes every codeword, agrees with the
-    staged engine on the decisions and tracks the f64 NMSE."""
+    """Designs where AMP decodes (L=512, M=512, R=1.2, w=2^19; and the C2
+    geometry at R=1.3, n=7089, whose 14 needed indices per thread put two X
+    slots in registers; with flat power n=6144 does not decode at any P, see
+    the R=1.5 test below): the per-codeword engine decodes every codeword,
+    agrees with the staged engine on the decisions and tracks the f64 NMSE."""
     M = 512
     n = int(round(L * 9 / R))
     W = np.array(P)
