@@ -255,8 +255,14 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
         for (int k = 0; k < CW_CO; ++k) {
             float zn = yv[k];
             if (have_beta) {  // Onsager residual, sparc.py:943-946
-                const cx<float> ha = ia[k] < CW_KL * CW_THREADS ? Xl[ia[k]] : d[ia[k] - CW_KL * CW_THREADS];
-                const cx<float> hb = ib[k] < CW_KL * CW_THREADS ? Xl[ib[k]] : d[ib[k] - CW_KL * CW_THREADS];
+                cx<float> ha, hb;
+                if constexpr (KT > CW_KL) {
+                    ha = ia[k] < CW_KL * CW_THREADS ? Xl[ia[k]] : d[ia[k] - CW_KL * CW_THREADS];
+                    hb = ib[k] < CW_KL * CW_THREADS ? Xl[ib[k]] : d[ib[k] - CW_KL * CW_THREADS];
+                } else {
+                    ha = Xl[ia[k]];
+                    hb = Xl[ib[k]];
+                }
                 float r = 0.f;
                 r += (c1[k].x * ha.x - c1[k].y * ha.y) + (c2[k].x * hb.x + c2[k].y * hb.y);
                 zn = (yv[k] - r) + bco * zv[k];
@@ -293,9 +299,8 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
         if (i < tb.n) zl[i] = zr[k] / phf;
     }
     __syncthreads();
-#pragma unroll
-    for (int j = 0; j < KT; ++j) {  // G by slot (unused terms: index 0, coefficient 0)
-        const int c = j * CW_THREADS + tid;
+    // G by slot (unused terms: index 0, coefficient 0)
+    for (int c = tid; c < CW_KL * CW_THREADS; c += CW_THREADS) {
         const int4 gi = reinterpret_cast<const int4 *>(tb.gi)[c];
         const float4 ga = reinterpret_cast<const float4 *>(tb.gc)[2 * c];
         const float4 gb = reinterpret_cast<const float4 *>(tb.gc)[2 * c + 1];
@@ -312,8 +317,30 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
         v = zl[gi.w];
         a.x += gb.z * v;
         a.y += gb.w * v;
-        if (j < CW_KL) Xl[c] = a;
-        else Xr[j < CW_KL ? 0 : j - CW_KL] = a;
+        Xl[c] = a;
+    }
+    if constexpr (KT > CW_KL) {
+#pragma unroll
+        for (int j = CW_KL; j < KT; ++j) {
+            const int c = j * CW_THREADS + tid;
+            const int4 gi = reinterpret_cast<const int4 *>(tb.gi)[c];
+            const float4 ga = reinterpret_cast<const float4 *>(tb.gc)[2 * c];
+            const float4 gb = reinterpret_cast<const float4 *>(tb.gc)[2 * c + 1];
+            cx<float> a{0.f, 0.f};
+            float v = zl[gi.x];
+            a.x += ga.x * v;
+            a.y += ga.y * v;
+            v = zl[gi.y];
+            a.x += ga.z * v;
+            a.y += ga.w * v;
+            v = zl[gi.z];
+            a.x += gb.x * v;
+            a.y += gb.y * v;
+            v = zl[gi.w];
+            a.x += gb.z * v;
+            a.y += gb.w * v;
+            Xr[j - CW_KL] = a;
+        }
     }
     __syncthreads();
     CW_TP(2);

@@ -943,8 +943,7 @@ static int decode_regular(sg_amp_plan *p, const void *d_y, int B, const int32_t 
         // engine spreads the active ones over every CU.  Both keep the same
         // state (s in class order, section statistics, scalars), so the
         // switch is seamless.
-        const bool poll = cw && !cw_forced ? (t % 2 == 1) : (t % 4 == 3);
-        if (poll && t + 1 < t_max - 1 && !tb.skip) {
+        if (t % 4 == 3 && t + 1 < t_max - 1 && !tb.skip) {
             SG_HIP(hipMemcpyAsync(act.data(), p->ws_active, sizeof(int32_t) * B, hipMemcpyDeviceToHost, s));
             SG_HIP(hipStreamSynchronize(s));
             int na = 0;
