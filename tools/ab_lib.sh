@@ -1,3 +1,8 @@
+#!/bin/bash
+# Same-box A/B of two library builds on the C2 bench line: the committed
+# build (ldpc_sparc_amd/_lib) against an alternative linked by hand into
+# ldpc_sparc_amd/_lib_alt (e.g. an older amp_cw.o), loaded through
+# LDPC_SPARC_AMD_LIB, interleaved twice.
 set -e
 cd "$GRAFT_REPO_ROOT"
 rm -rf gpurun_out/ab; mkdir -p gpurun_out/ab
