@@ -47,7 +47,7 @@ __device__ __forceinline__ double cw_block_sum(double v, double *red) {
 }
 
 constexpr int CW_LOG2P = 13, CW_P = 1 << CW_LOG2P, CW_EPT = CW_P / CW_THREADS;
-constexpr int CW_SN = 10;  // class entries per thread (host: largest class <= CW_SN * 1024)
+constexpr int CW_SN = 9;   // class entries per thread (host: largest class <= CW_SN * 1024)
 constexpr int CW_CO = 8;   // output rows per thread (host: n <= CW_CO * 1024)
 constexpr int CW_KL = 12;  // X / G slots per thread in LDS (96 KB); any further ones in registers
 

@@ -573,7 +573,7 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
     SG_TRY(upload_cx(p, &p->r_twa, twa));
     SG_TRY(upload_cx(p, &p->r_twb, twb));
     if (p->precision == SG_F32 && nT == 1 && P == (1 << 13) && Lblk <= CW_THREADS && n <= 8 * CW_THREADS &&
-        Q <= 64 && p->rmaxcls <= 10 * CW_THREADS && p->rimg == 2 * P && fpad(p->rmaxcls + 16) < p->rimg)
+        Q <= 64 && p->rmaxcls <= 9 * CW_THREADS && p->rimg == 2 * P && fpad(p->rmaxcls + 16) < p->rimg)
         SG_TRY(build_cw(p, row_k1[0], kptr[0], kk2[0], f_oa, f_ob, f_gi, f_gc));
     return SG_OK;
 }
