@@ -388,3 +388,30 @@ def test_cw_engine_c2_vs_oracle(monkeypatch):
     assert abs(int(tf[0]) - int(rt)) <= 1
     assert np.mean(mi[0] == np.argmax(rb.reshape(L, M), 1)) >= 0.99
     np.testing.assert_allclose(nm[0, :, 0], rn, atol=1e-3)
+
+
+def test_auto_engine_handover_matches_staged(monkeypatch):
+    """A batch that fills the CUs on a design where codewords stop early
+    (L=512, R=1.2): the automatic choice starts on the per-codeword engine and
+    hands the remaining iterations to the staged engine once half the batch
+    has stopped; decisions, stopping iterations and NMSE agree with the staged
+    engine alone."""
+    L, M, R = 512, 512, 1.2
+    n = int(round(L * 9 / R))
+    W = np.array(15.0)
+    o0, o1 = sparc.generate_ordering(W, n, L * M, 23)
+    B = 256  # one per CU on MI355X
+    rng = np.random.default_rng(31)
+    true = rng.integers(0, M, (B, L))
+    beta0 = np.zeros((B, L * M), np.float32)
+    beta0[np.arange(B)[:, None], np.arange(L) * M + true] = 1
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    Y = op.apply(beta0.astype(np.float64), False) + rng.standard_normal((B, n))
+    monkeypatch.delenv("SG_AMP_ENGINE", raising=False)
+    ma, ta, na, _ = sparc.amp_decode_batch(Y, op, 1.0, 25, true_idx=true, precision=_native.SG_F32)
+    assert _native.lib().sg_amp_plan_engine(op.plan(_native.SG_F32), B) == 2
+    monkeypatch.setenv("SG_AMP_ENGINE", "staged")
+    ms, ts, ns, _ = sparc.amp_decode_batch(Y, op, 1.0, 25, true_idx=true, precision=_native.SG_F32)
+    assert np.array_equal(ma, true) and np.array_equal(ms, true)
+    assert np.all(np.abs(ta - ts) <= 1)
+    np.testing.assert_allclose(na[:, :8], ns[:, :8], atol=1e-3)
