@@ -256,7 +256,10 @@ typedef struct sg_amp_plan sg_amp_plan;
  * in row-major order, whose row/column orders are order0[t][Mr] and
  * order1[t][Mc] exactly as generate_ordering (sparc.py:735-775) draws them
  * (Mr = n or n/Lr, Mc = L*M/Lc).  precision SG_F64 follows the reference's
- * double arithmetic; SG_F32 is the throughput path. */
+ * double arithmetic; SG_F32 is the throughput path.  A plan eligible for the
+ * per-codeword engine also holds a staged-engine plan at P = 16384, which
+ * decodes batches too small for the per-codeword engine (sg_amp_plan_info
+ * reports the per-codeword plan's P). */
 int sg_amp_plan_create(int ndim, const double *W, int Lr, int Lc, int L, int M, int n,
                        const uint32_t *order0, const uint32_t *order1, int precision,
                        sg_amp_plan **out);

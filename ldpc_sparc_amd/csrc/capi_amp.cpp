@@ -56,6 +56,11 @@ struct sg_amp_plan {
     // per-codeword engine (amp_cw.hip), built beside the regular tables when eligible
     bool cw = false;
     int cwKT = 0;
+    // A per-codeword plan uses P = 8192 for both engines; batches below one
+    // wave of the CUs decode on this companion plan instead: the staged
+    // engine at P = 16384 (17-21 % faster there, profiles/README.md)
+    bool no_cw = false;
+    sg_amp_plan *alt = nullptr;
     uint32_t *c_kt = nullptr;
     int32_t *c_oa = nullptr, *c_ob = nullptr, *c_gi = nullptr;
     void *c_gc = nullptr, *c_stw = nullptr;
@@ -359,7 +364,7 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
     // its tables; SG_AMP_ENGINE=staged at plan creation keeps P = 16384
     const char *eng = getenv("SG_AMP_ENGINE");
     if (p->precision == SG_F32 && nT == 1 && 2 * n <= 14 * CW_THREADS && Lblk <= CW_THREADS && N2 >= (1 << 14) &&
-        !(eng && std::strcmp(eng, "staged") == 0))
+        !p->no_cw && !(eng && std::strcmp(eng, "staged") == 0))
         Pmax = 8192;
     if (const char *e = getenv("SG_AMP_PMAX")) Pmax = std::max(8LL, std::min(16384LL, atoll(e)));  // tuning knob
     int P = (int)std::min<long long>(N2, Pmax);
@@ -631,6 +636,16 @@ static bool use_cw(const sg_amp_plan *p, int B) {
     return B >= cu && (double)B / ((double)waves * cu) >= 0.9;
 }
 
+// The plan a decode of B codewords runs on: the companion P = 16384 plan when
+// the automatic choice is the staged engine from the first iteration (the
+// SG_AMP_ENGINE overrides keep the plan itself, for same-table A/B tests).
+static sg_amp_plan *decode_plan(sg_amp_plan *p, int B) {
+    if (!p->alt) return p;
+    const char *e = std::getenv("SG_AMP_ENGINE");
+    if (e && (std::strcmp(e, "cw") == 0 || std::strcmp(e, "staged") == 0)) return p;
+    return use_cw(p, B) ? p : p->alt;
+}
+
 template <typename T>
 static RegBufs<T> rbufs(const sg_amp_plan *p, int B, const void *y) {
     RegBufs<T> bf;
@@ -726,7 +741,7 @@ static int build_block(sg_amp_plan *p, const uint32_t *order0, const uint32_t *o
 }
 
 static int build_plan(int ndim, const double *W, int Lr_in, int Lc_in, int L, int M, int n, const uint32_t *order0,
-                      const uint32_t *order1, int precision, sg_amp_plan **out) {
+                      const uint32_t *order1, int precision, bool no_cw, sg_amp_plan **out) {
     SG_CHECK_ARG(out && W && order0 && order1, "null argument");
     SG_CHECK_ARG(ndim >= 0 && ndim <= 2, "W.ndim must be 0, 1 or 2");
     SG_CHECK_ARG(precision == SG_F32 || precision == SG_F64, "precision must be SG_F32 or SG_F64");
@@ -747,6 +762,7 @@ static int build_plan(int ndim, const double *W, int Lr_in, int Lc_in, int L, in
     SG_CHECK_ARG(w >= 16 && w <= (1 << 23), "transform size w=%d outside [16, 2^23]", w);
     std::unique_ptr<sg_amp_plan> p(new sg_amp_plan());
     hipGetDevice(&p->device);
+    p->no_cw = no_cw;
     p->precision = precision; p->ndim = ndim; p->L = L; p->M = M; p->LM = (int)LM; p->n = n;
     p->Lr = Lr; p->Lc = Lc; p->Mr = Mr; p->Mc = Mc; p->w = w; p->N2 = w / 2;
     const int lg = ilog2(p->N2);
@@ -1120,11 +1136,22 @@ extern "C" {
 
 int sg_amp_plan_create(int ndim, const double *W, int Lr, int Lc, int L, int M, int n, const uint32_t *order0,
                        const uint32_t *order1, int precision, sg_amp_plan **out) {
-    return build_plan(ndim, W, Lr, Lc, L, M, n, order0, order1, precision, out);
+    sg_amp_plan *p = nullptr;
+    SG_TRY(build_plan(ndim, W, Lr, Lc, L, M, n, order0, order1, precision, false, &p));
+    if (p->cw) {
+        const int rc = build_plan(ndim, W, Lr, Lc, L, M, n, order0, order1, precision, true, &p->alt);
+        if (rc != SG_OK) {
+            sg_amp_plan_destroy(p);
+            return rc;
+        }
+    }
+    *out = p;
+    return SG_OK;
 }
 
 int sg_amp_plan_destroy(sg_amp_plan *p) {
     if (!p) return SG_OK;
+    sg_amp_plan_destroy(p->alt);
     plan_free_ws(p);
     for (void *a : p->allocs) hipFree(a);
     if (p->tprof) hipFree(p->tprof);
@@ -1160,6 +1187,7 @@ int sg_amp_decode_device(sg_amp_plan *p, const void *d_y, int B, const int32_t *
     SG_CHECK_ARG(B >= 0, "negative batch");
     if (B == 0) return SG_OK;
     SG_CHECK_ARG(d_y, "d_y is NULL");
+    p = sg::decode_plan(p, B);
     SG_TRY(ensure_device());
     SG_HIP(hipSetDevice(p->device));
     hipStream_t s = pick_stream(stream);
@@ -1177,6 +1205,7 @@ int sg_amp_decode(sg_amp_plan *p, const double *y, int B, const int32_t *true_id
     if (B == 0) return SG_OK;
     SG_CHECK_ARG(y && map_idx && t_final && nmse && psi, "null host buffer");
     SG_CHECK_ARG(t_max > 1, "t_max must be > 1 (sparc.py:168)");
+    p = sg::decode_plan(p, B);
     SG_TRY(ensure_device());
     SG_HIP(hipSetDevice(p->device));
     hipStream_t s = lib_stream();
@@ -1246,6 +1275,7 @@ int sg_amp_encode_device(sg_amp_plan *p, const int32_t *d_idx, int B, void *d_x,
 int sg_amp_stage_profile(sg_amp_plan *p, int kernel, double *mean_cycles, int *nphases) {
     SG_CHECK_ARG(p && mean_cycles && nphases && (kernel == 0 || kernel == 1), "bad argument");
     *nphases = 0;
+    if (!p->tprof && p->alt) p = p->alt;  // a small batch ran on the companion plan
     if (!p->tprof) return SG_OK;
     std::vector<uint64_t> h(p->tprof_items * 8);
     SG_HIP(hipDeviceSynchronize());
@@ -1265,6 +1295,7 @@ int sg_amp_stage_profile(sg_amp_plan *p, int kernel, double *mean_cycles, int *n
 
 int sg_amp_stage_raw(sg_amp_plan *p, int kernel, uint64_t *out, size_t *items) {
     SG_CHECK_ARG(p && items && (kernel == 0 || kernel == 1), "bad argument");
+    if (!p->tprof && p->alt) p = p->alt;
     *items = p->tprof ? p->tprof_items : 0;
     if (!p->tprof || !out) return SG_OK;
     const size_t ni = p->tprof_items;

@@ -11,6 +11,8 @@ Bars (stated tolerances):
   * full size (L=1024, M=512, w=2^20): operators as above; R=1.3 codewords
     decode with BER 0; NMSE trajectory tracks the CPU restatement.
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -410,6 +412,37 @@ def test_auto_engine_handover_matches_staged(monkeypatch):
     monkeypatch.delenv("SG_AMP_ENGINE", raising=False)
     ma, ta, na, _ = sparc.amp_decode_batch(Y, op, 1.0, 25, true_idx=true, precision=_native.SG_F32)
     assert _native.lib().sg_amp_plan_engine(op.plan(_native.SG_F32), B) == 2
+    monkeypatch.setenv("SG_AMP_ENGINE", "staged")
+    ms, ts, ns, _ = sparc.amp_decode_batch(Y, op, 1.0, 25, true_idx=true, precision=_native.SG_F32)
+    assert np.array_equal(ma, true) and np.array_equal(ms, true)
+    assert np.all(np.abs(ta - ts) <= 1)
+    np.testing.assert_allclose(na[:, :8], ns[:, :8], atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_small_batch_runs_on_companion_plan(monkeypatch):
+    """Below one wave of the CUs the automatic choice is the staged engine;
+    a per-codeword plan (P = 8192) then decodes on its companion plan at
+    P = 16384.  Decisions, stopping iterations and NMSE agree with the staged
+    engine on the P = 8192 tables (SG_AMP_ENGINE=staged keeps the plan)."""
+    L, M, R = 512, 512, 1.2
+    n = int(round(L * 9 / R))
+    W = np.array(15.0)
+    o0, o1 = sparc.generate_ordering(W, n, L * M, 29)
+    B = 24
+    rng = np.random.default_rng(37)
+    true = rng.integers(0, M, (B, L))
+    beta0 = np.zeros((B, L * M), np.float32)
+    beta0[np.arange(B)[:, None], np.arange(L) * M + true] = 1
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    Y = op.apply(beta0.astype(np.float64), False) + rng.standard_normal((B, n))
+    monkeypatch.delenv("SG_AMP_ENGINE", raising=False)
+    plan = op.plan(_native.SG_F32)
+    P = ctypes.c_int()
+    _native.lib().sg_amp_plan_info(plan, None, None, None, None, ctypes.byref(P), None)
+    assert P.value == 8192
+    assert _native.lib().sg_amp_plan_engine(plan, B) == 1
+    ma, ta, na, _ = sparc.amp_decode_batch(Y, op, 1.0, 25, true_idx=true, precision=_native.SG_F32)
     monkeypatch.setenv("SG_AMP_ENGINE", "staged")
     ms, ts, ns, _ = sparc.amp_decode_batch(Y, op, 1.0, 25, true_idx=true, precision=_native.SG_F32)
     assert np.array_equal(ma, true) and np.array_equal(ms, true)
