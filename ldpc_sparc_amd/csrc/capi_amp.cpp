@@ -942,6 +942,8 @@ static int decode_regular(sg_amp_plan *p, const void *d_y, int B, const int32_t 
     bool cw = std::is_same<T, float>::value && use_cw(p, B);
     const char *eng = std::getenv("SG_AMP_ENGINE");
     const bool cw_forced = eng && std::strcmp(eng, "cw") == 0;
+    double handover = 0.5;  // active fraction below which the staged engine takes over
+    if (const char *h = std::getenv("SG_AMP_HANDOVER")) handover = atof(h);  // tuning knob
     for (int t = 0; t < t_max - 1; ++t) {
         if constexpr (std::is_same<T, float>::value) {
             if (cw) SG_TRY(cw_launch_iter(ctables(p), bf, sc, pr, t, s));
@@ -965,7 +967,7 @@ static int decode_regular(sg_amp_plan *p, const void *d_y, int B, const int32_t 
             int na = 0;
             for (int b = 0; b < B; ++b) na += act[b] != 0;
             if (na == 0) break;
-            if (cw && !cw_forced && 2 * na < B) cw = false;
+            if (cw && !cw_forced && na < handover * B) cw = false;
         }
     }
     SG_HIP(hipMemsetAsync(p->ws_argmax, 0x7f, sizeof(int32_t) * B * p->L, s));
