@@ -19,15 +19,27 @@ algorithmic bytes per codeword-iteration 4*(2LM+4n); the BP kernel with
 4*(4*Nmsg+N) bytes per codeword-iteration.  Kernel durations come from HIP
 events recorded on the library stream around every launch in the timed region.
 
-CPU baseline: the CPU restatement in oracle/ (test infrastructure; here only as
-the timed baseline) on one host core, on a bounded sample (rank 0, N=1 only).
+Roofline: the C2 headline leads with the binding bound, the f32 vector ALUs
+(SURVEY.md 8(d) flops per codeword-iteration; the FFTs run on the VALU), with
+the HBM bound beside it; BP leads with the LDS bound (its messages never leave
+LDS), HBM beside it.
+
+CPU baseline: the CPU restatements in oracle/ (test infrastructure; here only
+as the timed baseline) on one single-threaded process per host core
+(oracle/cpu_pool.py, OMP_NUM_THREADS=1, core count stated), over the same
+received words the GPU decoded, bounded in time (rank 0, N=1 only).  The
+decisions of both are compared over the whole sample.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-       (N>1: launched by torch.distributed.run, one process per GPU).
+       N>1 without torch.distributed.run's environment: bench.py starts
+       torch.distributed.run itself (one process per GPU) before touching the
+       GPU, and exits non-zero when fewer than N GPUs are visible.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -65,11 +77,77 @@ def parse():
     ap.add_argument("--concat-batch", type=int, default=256)
     ap.add_argument("--concat-steps", type=int, default=2)
     ap.add_argument("--concat-ebn0", type=float, default=4.0)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0,
-                    help="approximate CPU-baseline sample length (0 disables)")
+    ap.add_argument("--cpu-seconds", type=float, default=60.0,
+                    help="wall-time cap of the C2 CPU-baseline sample (the other legs scale from it; 0 disables)")
+    ap.add_argument("--cpu-procs", type=int, default=0,
+                    help="CPU-baseline processes (default: the host cores available, at most 16)")
+    ap.add_argument("--rendezvous-check", action="store_true",
+                    help="launch/rendezvous only (no GPU): rank 0 prints the ranks that joined")
     ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
     ap.add_argument("--seed", type=int, default=1, help="Philox key of the synthetic inputs (stream = rank)")
     return ap.parse_args()
+
+
+# Library knobs that change what the timed region runs (engine forcing, tuning,
+# diagnostics).  A benchmark runs the shipped defaults only.
+ENGINE_ENV_PREFIX = "SG_AMP_"
+
+
+def guard_env():
+    bad = sorted(k for k in os.environ if k.startswith(ENGINE_ENV_PREFIX))
+    if bad:
+        sys.stderr.write("bench.py: refusing to run with engine knobs set (%s): the benchmark measures the shipped "
+                         "defaults; unset them\n" % ", ".join(bad))
+        sys.exit(3)
+
+
+def visible_gpus():
+    """GPUs this process could use, counted without initialising the GPU
+    (torch.cuda.device_count() does not initialise HIP on this image)."""
+    import torch
+    return int(torch.cuda.device_count())
+
+
+def maybe_spawn(args):
+    """--gpus N > 1 outside torch.distributed.run: start it (one rank per GPU)
+    as a child process and exit with its code.  Nothing here touches the GPU,
+    so the parent never holds GPU state while the ranks run."""
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is not None:
+        if int(world_env) != args.gpus:
+            sys.stderr.write(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}\n")
+            sys.exit(2)
+        return
+    if args.gpus <= 1:
+        return
+    if not args.rendezvous_check:
+        ng = visible_gpus()
+        if ng < args.gpus:
+            sys.stderr.write(f"bench.py: --gpus {args.gpus} but only {ng} GPU(s) visible; refusing to run "
+                             f"fewer ranks\n")
+            sys.exit(2)
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    sys.exit(subprocess.run(cmd, env=env).returncode)
+
+
+def rendezvous_check(d):
+    """--rendezvous-check: every rank joins, barriers, and reports its rank;
+    rank 0 prints the ranks that joined (CPU only, no GPU call)."""
+    ranks = [d.rank]
+    if d.world > 1:
+        obj = [None] * d.world
+        d.dist.all_gather_object(obj, d.rank)
+        ranks = obj
+    d.barrier()
+    if d.rank == 0:
+        print(json.dumps({"rendezvous": "ok", "n_ranks": len(ranks), "ranks": sorted(ranks),
+                          "world_size": d.world}), flush=True)
+    d.close()
 
 
 class Dist:
@@ -140,15 +218,20 @@ class HostCounterComm:
         pass
 
 
+PMC_TRAFFIC_FILES = ("r02_pmc_traffic_bench.json", "r01_pmc_traffic_bench.json")
+
+
 def pmc_traffic(section, field):
     """HBM bytes per unit from the committed PMC passes of tools/pmc_bench.sh
-    (profiles/r01_pmc_traffic_bench.json), or None."""
-    path = os.path.join(REPO, "profiles", "r01_pmc_traffic_bench.json")
-    try:
-        with open(path) as f:
-            return json.load(f)[section][field]
-    except (OSError, KeyError, ValueError):
-        return None
+    over this bench (profiles/r02_pmc_traffic_bench.json, else the round-1
+    file): (value, file) or (None, None)."""
+    for name in PMC_TRAFFIC_FILES:
+        try:
+            with open(os.path.join(REPO, "profiles", name)) as f:
+                return json.load(f)[section][field], name
+        except (OSError, KeyError, ValueError):
+            continue
+    return None, None
 
 
 # ------------------------------------------------------------------ AMP (C2)
@@ -195,7 +278,7 @@ def amp_step(st, args, comm):
         comm.allreduce_sum_i64(st["d_cnt"], 4)
 
 
-def amp_decodable(args, d, comm, cpu_seconds):
+def amp_decodable(args, d, comm, cpu_seconds, procs):
     """SURVEY.md 8(d) C2 companion: the same engine at R=1.3 (n=7089), where AMP
     decodes in 14-18 iterations, so the BER comparison with the CPU
     restatement is made on codewords that mostly decode."""
@@ -219,50 +302,50 @@ def amp_decodable(args, d, comm, cpu_seconds):
            "codeword_errors": int(cnt[2]),
            "ber": float(cnt[1]) / (d.world * st["B"] * st["L"] * st["logM"])}
     if cpu_seconds > 0:
-        out["cpu_baseline"] = amp_cpu_baseline(st, a, cpu_seconds)
+        out["cpu_baseline"] = amp_cpu_baseline(st, a, cpu_seconds, procs)
     return out
 
 
-def amp_cpu_baseline(st, args, seconds):
-    """oracle/sparc_ref.py (scipy DCT operators, float128 softmax as the
-    reference) on one core, on as many codewords of the same batch as fit."""
-    from oracle import sparc_ref
-    L, M, n = st["L"], st["M"], st["n"]
-    Ab, Az = sparc_ref.dct_operators(st["W"], L, M, n, st["o0"], st["o1"])
-    # the same received words and message indices the GPU decodes
+def popcount32(a):
+    a = np.asarray(a, np.uint32)
+    return int(np.unpackbits(a.view(np.uint8)).sum())
+
+
+def amp_cpu_baseline(st, args, seconds, procs):
+    """oracle/sparc_ref.py (scipy fftpack DCT operators, float128 softmax, as
+    sparc.py:883-999) on `procs` single-threaded processes over the same
+    received words the GPU decoded (the whole batch unless the wall-time cap
+    cuts it), with the GPU's decisions compared codeword by codeword."""
+    from oracle import cpu_pool
+    L, M, n, B = st["L"], st["M"], st["n"], st["B"]
     dt = np.float32 if st["prec"] == _native.SG_F32 else np.float64
-    Y = st["d_y"].download(np.zeros((st["B"], n), dt)).astype(np.float64)
-    true = st["d_true"].download(np.zeros((st["B"], L), np.int32))
-    gmap = st["d_map"].download(np.zeros((st["B"], L), np.int32))  # the GPU's decisions, same codewords
-    t0 = time.perf_counter()
-    done = iters = 0
-    cbits = gbits = csec = gsec = same = 0
-    while True:
-        b = done
-        beta0 = np.zeros(L * M)
-        beta0[np.arange(L) * M + true[b]] = 1.0
-        bh, tf, _, _ = sparc_ref.amp(Y[b], st["W"], L, M, n, 1.0, args.t_max, Ab, Az, beta0)
-        cidx = np.argmax(bh.reshape(L, M), 1)
-        cbits += int(sum(bin(int(v)).count("1") for v in (cidx ^ true[b])))
-        gbits += int(sum(bin(int(v)).count("1") for v in (gmap[b] ^ true[b])))
-        csec += int((cidx != true[b]).sum())
-        gsec += int((gmap[b] != true[b]).sum())
-        same += int((cidx == gmap[b]).sum())
-        done += 1
-        iters += tf
-        el = time.perf_counter() - t0
-        if el >= seconds or done >= st["B"]:
-            break
-    nb = done * L * st["logM"]
-    return {"value": done / el, "unit": "codewords/s", "cores": 1, "kind": "port",
-            "sample": f"{done} C2 codewords (R={args.rate}, t_max={args.t_max}, {iters} AMP "
-                      f"iterations, {el:.1f} s) decoded by oracle/sparc_ref.py (numpy/scipy "
-                      f"fftpack DCT, float128 softmax) on 1 host core",
-            "ber_match": {"codewords": done, "cpu_ber": cbits / nb, "gpu_ber": gbits / nb,
-                          "cpu_ser": csec / (done * L), "gpu_ser": gsec / (done * L),
-                          "identical_section_decisions": same / (done * L),
+    Y = st["d_y"].download(np.zeros((B, n), dt)).astype(np.float64)
+    true = st["d_true"].download(np.zeros((B, L), np.int32))
+    gmap = st["d_map"].download(np.zeros((B, L), np.int32))  # the GPU's decisions, same codewords
+    gtf = st["d_tf"].download(np.zeros(B, np.int32))
+    res, el = cpu_pool.amp_decode(procs, st["W"], L, M, n, st["o0"], st["o1"], Y, true, args.t_max, seconds)
+    done = sorted(res)
+    nd = len(done)
+    cmap = np.stack([res[b][0] for b in done])
+    ctf = np.array([res[b][1] for b in done])
+    g, t = gmap[done], true[done]
+    csec, gsec = (cmap != t), (g != t)
+    nb = nd * L * st["logM"]
+    iters = int(ctf.sum())
+    return {"value": nd / el, "unit": "codewords/s", "cores": procs, "kind": "port",
+            "sample": f"{nd} of the {B} C2 codewords the GPU decoded (R={args.rate}, t_max={args.t_max}, {iters} AMP "
+                      f"iterations, {el:.1f} s wall) by oracle/sparc_ref.py (numpy/scipy fftpack DCT, float128 "
+                      f"softmax), one single-threaded process per core on {procs} host cores",
+            "ber_match": {"codewords": nd,
+                          "cpu_ber": popcount32(cmap ^ t) / nb, "gpu_ber": popcount32(g ^ t) / nb,
+                          "cpu_ser": float(csec.mean()), "gpu_ser": float(gsec.mean()),
+                          "cpu_fer": float(csec.any(1).mean()), "gpu_fer": float(gsec.any(1).mean()),
+                          "identical_section_decisions": float((cmap == g).mean()),
+                          "identical_codeword_decisions": float((cmap == g).all(1).mean()),
+                          "t_final_equal": float((ctf == gtf[done]).mean()),
+                          "t_final_max_abs_diff": int(np.abs(ctf - gtf[done]).max()),
                           "note": "the GPU's decisions for the same received words (f32 engine vs the f64/"
-                                  "float128 CPU restatement)"}}
+                                  "float128 CPU restatement), over every codeword of the CPU sample"}}
 
 
 # ------------------------------------------------------------------ BP (C3)
@@ -293,42 +376,35 @@ def bp_step(st):
                                                   st["d_it"].ptr, st["B"], c.K, st["d_cnt"].ptr, None))
 
 
-def bp_cpu_baseline(st, seconds):
-    """oracle/bp_oracle.c min-sum (reference c_ldpc.c with the loop index
-    corrected) on one host core."""
-    from oracle import bp
+def bp_cpu_baseline(st, seconds, procs):
+    """oracle/bp_oracle.c min-sum (reference c_ldpc.c:339-381 with the loop
+    index corrected) on `procs` single-threaded processes, over every codeword
+    the GPU decoded unless the wall-time cap cuts the sample."""
+    from oracle import cpu_pool
     c = st["c"]
     gapp = st["d_app"].download(np.zeros((st["B"], c.N), np.float32))  # the GPU's output, same codewords
-    t0 = time.perf_counter()
-    done = 0
-    cerr = gerr = cfe = gfe = same = 0
-    while True:
-        chunk = st["ch"][done:done + 64]
-        app, _ = bp.decode_batch("minsum", chunk, c.vdeg, c.cdeg, c.intrlv, 50, 0.7)
-        x = st["X"][done:done + len(chunk)]
-        ch_, gh = (app < 0).astype(np.int64), (gapp[done:done + len(chunk)] < 0).astype(np.int64)
-        cerr += int((ch_[:, :c.K] != x[:, :c.K]).sum())
-        gerr += int((gh[:, :c.K] != x[:, :c.K]).sum())
-        cfe += int((ch_[:, :c.K] != x[:, :c.K]).any(1).sum())
-        gfe += int((gh[:, :c.K] != x[:, :c.K]).any(1).sum())
-        same += int((ch_ == gh).all(1).sum())
-        done += len(chunk)
-        el = time.perf_counter() - t0
-        if el >= seconds or done >= st["B"]:
-            break
-    return {"value": done / el, "unit": "codewords/s", "cores": 1, "kind": "port",
-            "sample": f"{done} C3 codewords (802.11n r1/2 z=81, min-sum, 50 it, Eb/N0 "
-                      f"{st.get('ebn0')} dB) by oracle/bp_oracle.c on 1 host core",
-            "ber_match": {"codewords": done, "cpu_ber": cerr / (done * c.K), "gpu_ber": gerr / (done * c.K),
-                          "cpu_fer": cfe / done, "gpu_fer": gfe / done,
-                          "identical_codeword_decisions": same / done,
+    git = st["d_it"].download(np.zeros(st["B"], np.int32))
+    app, it, done, el = cpu_pool.bp_decode(procs, "minsum", st["ch"], c.vdeg, c.cdeg, c.intrlv, 50, 0.7,
+                                           deadline_s=seconds)
+    nd = int(done.sum())
+    x = st["X"][done][:, :c.K]
+    ch_, gh = (app[done] < 0).astype(np.int64), (gapp[done] < 0).astype(np.int64)
+    ce, ge = (ch_[:, :c.K] != x), (gh[:, :c.K] != x)
+    return {"value": nd / el, "unit": "codewords/s", "cores": procs, "kind": "port",
+            "sample": f"{nd} of the {st['B']} C3 codewords the GPU decoded (802.11n r1/2 z=81, min-sum, 50 it, "
+                      f"Eb/N0 {st.get('ebn0')} dB, {el:.1f} s wall) by oracle/bp_oracle.c, one single-threaded "
+                      f"process per core on {procs} host cores",
+            "ber_match": {"codewords": nd, "cpu_ber": float(ce.sum()) / (nd * c.K), "gpu_ber": float(ge.sum()) / (nd * c.K),
+                          "cpu_fer": float(ce.any(1).mean()), "gpu_fer": float(ge.any(1).mean()),
+                          "identical_codeword_decisions": float((ch_ == gh).all(1).mean()),
+                          "identical_iteration_counts": float((it[done] == git[done]).mean()),
                           "note": "information-bit errors of the GPU (f32) and the CPU restatement (f64) on the same "
-                                  "channel LLRs"}}
+                                  "channel LLRs, over every codeword of the CPU sample"}}
 
 
 # ------------------------------------------------------------------ spatially coupled (C4)
 
-def sc_bench(args, d, comm, cpu_seconds):
+def sc_bench(args, d, comm, cpu_seconds, procs):
     """C4 (BASELINE.json configs[3], sparc_demo_sc_decode_wave): spatially
     coupled SPARC, omega=6, Lambda=32 (W 37x32, 192 transforms of w=2^15),
     L=1024, M=512, R=1.5 (n=6142), P=15, sigma^2=1, t_max=40; block engine
@@ -379,6 +455,7 @@ def sc_bench(args, d, comm, cpu_seconds):
     cw_it = int(tf.sum()) * args.sc_steps
     kms = sum(ph.get(k, (0.0, 0))[0] for k in AMP_PHASES)
     w = int(op.w)
+    sc_traffic, sc_tfile = pmc_traffic("sc", "hbm_bytes_per_codeword_iteration_approx")
     flops = 2 * int(np.count_nonzero(W)) * 2.5 * w * np.log2(w) + 20 * L * M  # per codeword-iteration
     ach = flops * cw_it / (kms * 1e-3) / 1e12 if kms else None
     out = {"workload": "C4: spatially coupled SPARC (omega=6, Lambda=32, W 37x32, 192 transforms of w=2^15), "
@@ -388,9 +465,9 @@ def sc_bench(args, d, comm, cpu_seconds):
            "ser": float(cnt[0]) / (d.world * B * L),
            "roofline": {"bound": "valu-f32", "achieved": ach, "peak": VALU_PEAK_TFS, "unit": "TFLOP/s",
                         "frac": ach / VALU_PEAK_TFS if ach else None,
-                        "traffic": pmc_traffic("sc", "hbm_bytes_per_codeword_iteration_approx"),
+                        "traffic": sc_traffic,
                         "traffic_unit": "HBM bytes per codeword-iteration, block-engine kernels (PMC, "
-                                        "profiles/r01_pmc_traffic_bench.json)",
+                                        f"profiles/{sc_tfile})",
                         "kernel": "blk_ab + blk_g + blk_az + control (amp_block.hip)",
                         "algorithmic_flops_per_codeword_iteration": flops,
                         "note": "2 nT transforms x 2.5 w log2 w + 20 L M per codeword-iteration; each transform "
@@ -398,25 +475,23 @@ def sc_bench(args, d, comm, cpu_seconds):
                         "kernel_ms": {k: round(v[0], 3) for k, v in ph.items()},
                         "launches": {k: v[1] for k, v in ph.items()}}}
     if d.rank == 0 and d.world == 1 and cpu_seconds > 0:
-        from oracle import sparc_ref
-        Ab, Az = sparc_ref.dct_operators(W, L, M, n, o0, o1)
+        from oracle import cpu_pool
         Y = d_y.download(np.zeros((B, n), np.float32)).astype(np.float64)
         true = d_true.download(np.zeros((B, L), np.int32))
-        t0 = time.perf_counter()
-        done = iters = 0
-        while True:
-            beta0 = np.zeros(L * M)
-            beta0[np.arange(L) * M + true[done]] = 1.0
-            _, t_f, _, _ = sparc_ref.amp(Y[done], W, L, M, n, 1.0, t_max, Ab, Az, beta0)
-            done += 1
-            iters += t_f
-            cel = time.perf_counter() - t0
-            if cel >= cpu_seconds or done >= B:
-                break
-        out["cpu_baseline"] = {"value": done / cel, "unit": "codewords/s", "cores": 1, "kind": "port",
-                               "sample": f"{done} C4 codewords ({iters} AMP iterations, {cel:.1f} s) decoded by "
-                                         "oracle/sparc_ref.py (scipy fftpack DCT per block, float128 softmax) "
-                                         "on 1 host core"}
+        gmap = d_map.download(np.zeros((B, L), np.int32))
+        res, cel = cpu_pool.amp_decode(procs, W, L, M, n, o0, o1, Y, true, t_max, cpu_seconds)
+        done = sorted(res)
+        cmap = np.stack([res[b][0] for b in done])
+        ctf = np.array([res[b][1] for b in done])
+        out["cpu_baseline"] = {"value": len(done) / cel, "unit": "codewords/s", "cores": procs, "kind": "port",
+                               "sample": f"{len(done)} C4 codewords ({int(ctf.sum())} AMP iterations, {cel:.1f} s "
+                                         "wall) decoded by oracle/sparc_ref.py (scipy fftpack DCT per block, float128 "
+                                         f"softmax), one single-threaded process per core on {procs} host cores",
+                               "ber_match": {"codewords": len(done),
+                                             "cpu_ser": float((cmap != true[done]).mean()),
+                                             "gpu_ser": float((gmap[done] != true[done]).mean()),
+                                             "identical_section_decisions": float((cmap == gmap[done]).mean()),
+                                             "t_final_equal": float((ctf == tf[done]).mean())}}
     return out
 
 
@@ -469,20 +544,55 @@ def concat_bench(args, d):
                          "launches": {k: v[1] for k, v in ph.items()}}}
 
 
+LDS_READ_B32 = 128   # B/clk/CU, ds_read_b32 (MI355X_MICROARCH.md LDS table)
+LDS_WRITE_B32 = 64   # B/clk/CU, ds_write_b32
+CLOCK_GHZ = 2.4      # max shader clock, MI355X_MICROARCH.md chip table
+
+
+def bp_lds_peak_gbs(ncu):
+    """LDS peak for BP's access mix: equal read and write bytes of f32 messages
+    (ds_read_b32 at 128 B/clk/CU, ds_write_b32 at 64), i.e. the harmonic mean
+    85.3 B/clk/CU over every CU at the maximum clock."""
+    per_cu = 2.0 / (1.0 / LDS_READ_B32 + 1.0 / LDS_WRITE_B32)
+    return per_cu * ncu * CLOCK_GHZ
+
+
 def main():
     args = parse()
+    guard_env()
+    maybe_spawn(args)  # --gpus N > 1 outside torch.distributed.run: re-launched as N ranks, exits
     d = Dist()
+    if args.rendezvous_check:
+        return rendezvous_check(d)
     _native.require_gpu()
     ndev = _native.device_count()
+    if d.world > 1 and d.world > ndev and os.environ.get("BENCH_REHEARSAL") != "1":
+        sys.stderr.write(f"bench.py: {d.world} ranks but {ndev} GPU(s) visible (BENCH_REHEARSAL=1 shares one GPU "
+                         "with host-side counters, for rehearsals only)\n")
+        sys.exit(2)
     _native.check(_native.lib().sg_set_device(d.local % max(ndev, 1)))
     comm = None
     counter_path = "none"
+    rccl_ranks = 1
     if d.world > 1:
-        if d.world > ndev and os.environ.get("BENCH_FORCE_RCCL") != "1":
-            comm, counter_path = HostCounterComm(d), "gloo (ranks share a GPU: rehearsal only)"
+        if d.world > ndev:
+            comm, counter_path = HostCounterComm(d), "gloo (BENCH_REHEARSAL: ranks share a GPU)"
         else:
             uid = d.bcast_bytes(_native.Comm.unique_id() if d.rank == 0 else None)
             comm, counter_path = _native.Comm(d.world, d.rank, uid), "rccl"
+            rccl_ranks, dev = comm.info()
+            # every rank on its own GPU: count the distinct (host, device) pairs
+            import torch
+            obj = [None] * d.world
+            d.dist.all_gather_object(obj, (socket.gethostname(), dev))
+            if len(set(obj)) != d.world or rccl_ranks != d.world:
+                sys.stderr.write(f"bench.py: RCCL sees {rccl_ranks} ranks on {len(set(obj))} distinct GPUs, "
+                                 f"expected {d.world}\n")
+                sys.exit(2)
+    procs = args.cpu_procs or 0
+    if d.rank == 0 and d.world == 1 and args.cpu_seconds > 0 and not procs:
+        from oracle import cpu_pool
+        procs = cpu_pool.host_cores()
 
     st = amp_setup(args, d.rank)
     for _ in range(args.warmup):
@@ -502,25 +612,27 @@ def main():
     tf = st["d_tf"].download(np.zeros(st["B"], np.int32))
     cw_it = int(tf.sum()) * args.steps  # executed codeword-iterations on this rank
     amp_ms = sum(phases.get(p, (0.0, 0))[0] for p in AMP_PHASES)
+    launches = sum(phases.get(p, (0.0, 0))[1] for p in AMP_PHASES)
     bytes_per_cwit = 4 * (2 * st["L"] * st["M"] + 4 * st["n"])
     w = int(st["op"].w)  # transform length (2^20 at C2)
     flops_per_cwit = 2 * 2.5 * w * np.log2(w) + 20 * st["L"] * st["M"]
-    achieved = bytes_per_cwit * cw_it / (amp_ms * 1e-3) / 1e9 if amp_ms > 0 else None
     total_cw = d.world * st["B"] * args.steps
     # the engine this batch ran on (2: per-codeword amp_cw.hip, 1: staged amp_fused.hip)
     engine = _native.lib().sg_amp_plan_engine(st["plan"], st["B"])
+    last = _native.amp_last_decode(st["plan"])
     engine_name = {1: "staged (amp_fused.hip)", 2: "per-codeword (amp_cw.hip)"}.get(engine, str(engine))
-    traffic = None
-    tfile = "r01_pmc_traffic_amp_c2_cw.json" if engine == 2 else "r01_pmc_traffic_amp_c2.json"
-    tpath = os.path.join(REPO, "profiles", tfile)
-    if os.path.exists(tpath):  # rocprofv3 --pmc passes of tools/pmc_traffic.py (same engine, B=256)
-        with open(tpath) as f:
-            traffic = json.load(f)["hbm_bytes_per_codeword_iteration"]
+    # rocprofv3 --pmc passes of tools/pmc_bench.sh over this bench command
+    traffic, tfile = pmc_traffic("amp", "hbm_bytes_per_codeword_iteration") if engine == 2 else (None, None)
+    cw_it_per_launch = cw_it / launches if launches else None
+    tflops = flops_per_cwit * cw_it / (amp_ms * 1e-3) / 1e12 if amp_ms > 0 else None
+    gbs = bytes_per_cwit * cw_it / (amp_ms * 1e-3) / 1e9 if amp_ms > 0 else None
+    kernel = ("cw_iter (one launch per AMP iteration of the batch)" if engine == 2 else
+              "one AMP iteration = " + "+".join(AMP_PHASES[:6]))
     out = {
         "metric": METRIC,
         "value": total_cw / el_max,
         "unit": "codewords/s",
-        "n_gpus": d.world,
+        "n_gpus": rccl_ranks if counter_path == "rccl" else d.world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": 1e3 * el_max / args.steps,
@@ -535,32 +647,35 @@ def main():
                    "awgn_var": 1.0, "t_max": args.t_max, "batch_per_gpu": st["B"],
                    "parallelism": f"mc-shard x{d.world} (independent codewords per GPU, "
                                   "RCCL all-reduce of error counters)",
-                   "counter_allreduce": counter_path},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-                     "traffic_unit": "HBM bytes per codeword-iteration (PMC FETCH_SIZE*2 + WRITE_SIZE, "
-                                     f"profiles/{tfile})",
-                     "engine": engine_name,
-                     "kernel": ("cw_iter (one launch per AMP iteration)" if engine == 2 else
-                                "one AMP iteration = " + "+".join(AMP_PHASES[:6])),
-                     "algorithmic_bytes_per_codeword_iteration": bytes_per_cwit,
-                     "codeword_iterations": cw_it,
+                   "counter_allreduce": counter_path, "rccl_ranks": rccl_ranks,
+                   "engine_env": {}, "engine": engine_name,
+                   "handover_iter": last["handover_iter"]},
+        "roofline": {"bound": "valu-f32", "achieved": tflops, "peak": VALU_PEAK_TFS, "unit": "TFLOP/s",
+                     "frac": tflops / VALU_PEAK_TFS if tflops else None,
+                     "traffic": traffic * cw_it_per_launch if (traffic and cw_it_per_launch) else None,
+                     "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE + WRITE_SIZE per codeword-iteration, "
+                                     f"profiles/{tfile}, x codeword-iterations per launch)",
+                     "traffic_per_codeword_iteration": traffic,
+                     "engine": engine_name, "kernel": kernel,
+                     "algorithmic_flops_per_codeword_iteration": flops_per_cwit,
+                     "codeword_iterations": cw_it, "codeword_iterations_per_launch": cw_it_per_launch,
                      "kernel_ms": {k: round(v[0], 3) for k, v in phases.items()},
-                     "launches": {k: v[1] for k, v in phases.items()}},
-        "roofline_flops": {"bound": "valu-f32", "achieved": flops_per_cwit * cw_it / (amp_ms * 1e-3) / 1e12
-                           if amp_ms > 0 else None, "peak": VALU_PEAK_TFS, "unit": "TFLOP/s",
-                           "frac": flops_per_cwit * cw_it / (amp_ms * 1e-3) / 1e12 / VALU_PEAK_TFS
-                           if amp_ms > 0 else None,
-                           "algorithmic_flops_per_codeword_iteration": flops_per_cwit,
-                           "note": "SURVEY.md 8(d): 2 transforms x 2.5 w log2 w + 20 L M; the FFTs run on the "
-                                   "vector ALUs (packed f32), so the f32 vector peak applies"},
+                     "launches": {k: v[1] for k, v in phases.items()},
+                     "note": "binding bound: SURVEY.md 8(d) flops (2 transforms x 2.5 w log2 w + 20 L M) at the "
+                             "f32 vector peak (the FFTs run on the VALU); achieved = flops x executed codeword-"
+                             "iterations / summed kernel time (HIP events on the library stream)"},
+        "roofline_hbm": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": gbs / HBM_PEAK_GBS if gbs else None,
+                         "algorithmic_bytes_per_codeword_iteration": bytes_per_cwit,
+                         "note": "SURVEY.md 8(d) 4(2LM + 4n) bytes per codeword-iteration over the same kernel time"},
         "amp": {"avg_iterations": float(tf.mean()), "section_errors": int(cnt[0]),
                 "bit_errors": int(cnt[1]), "codeword_errors": int(cnt[2]),
                 "ber": float(cnt[1]) / (d.world * st["B"] * st["L"] * st["logM"])},
     }
 
+    cpu_on = d.rank == 0 and d.world == 1 and args.cpu_seconds > 0
     if not args.no_r13:
-        out["amp_r13"] = amp_decodable(args, d, comm, args.cpu_seconds / 2 if d.world == 1 and d.rank == 0 else 0)
+        out["amp_r13"] = amp_decodable(args, d, comm, 0.75 * args.cpu_seconds if cpu_on else 0, procs)
 
     if not args.no_bp:
         bst = bp_setup(args, d.rank)
@@ -582,32 +697,46 @@ def main():
         c = bst["c"]
         exec_it = np.where(its < 50, its + 1, 50)  # executed iterations per codeword
         bp_ms = ph.get("bp_flood", (0.0, 0))[0]
+        cwit = exec_it.sum() * args.bp_steps
+        lds_bytes = 16 * c.Nmsg  # var pass reads + writes, check pass reads + writes every f32 message
+        lds_peak = bp_lds_peak_gbs(_native.cu_count())
+        lach = lds_bytes * cwit / (bp_ms * 1e-3) / 1e9 if bp_ms else None
         bbytes = 4 * (4 * c.Nmsg + c.N)
-        bach = bbytes * exec_it.sum() * args.bp_steps / (bp_ms * 1e-3) / 1e9 if bp_ms else None
+        bach = bbytes * cwit / (bp_ms * 1e-3) / 1e9 if bp_ms else None
+        hbm_meas, bp_tfile = pmc_traffic("bp", "hbm_bytes_per_codeword_iteration")
         out["bp"] = {"workload": "C3: 802.11n r1/2 z=81 (n=1944), min-sum (corr 0.7), max 50 it, "
                                  f"Eb/N0 {args.bp_ebn0} dB, random codewords",
                      "value": d.world * bst["B"] * args.bp_steps / bel, "unit": "codewords/s",
                      "batch_per_gpu": bst["B"], "avg_executed_iterations": float(exec_it.mean()),
                      "frame_errors": int(bcnt[1]), "bit_errors": int(bcnt[0]),
-                     "roofline": {"bound": "hbm", "achieved": bach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                  "frac": bach / HBM_PEAK_GBS if bach else None,
-                                  "traffic": pmc_traffic("bp", "hbm_bytes_per_codeword_iteration"),
-                                  "traffic_unit": "HBM bytes per codeword-iteration (PMC, messages stay in LDS; "
-                                                  "profiles/r01_pmc_traffic_bench.json)",
+                     "roofline": {"bound": "lds", "achieved": lach, "peak": lds_peak, "unit": "GB/s",
+                                  "frac": lach / lds_peak if lach else None,
+                                  "traffic": None,
                                   "kernel": "bp_flood_kernel<float, minsum>",
-                                  "algorithmic_bytes_per_codeword_iteration": bbytes,
-                                  "kernel_ms": bp_ms, "launches": ph.get("bp_flood", (0, 0))[1]}}
+                                  "algorithmic_lds_bytes_per_codeword_iteration": lds_bytes,
+                                  "kernel_ms": bp_ms, "launches": ph.get("bp_flood", (0, 0))[1],
+                                  "note": "the messages never leave LDS: 16 Nmsg bytes of f32 message reads and "
+                                          "writes per codeword-iteration against the LDS peak for that mix "
+                                          "(ds_read_b32 128 B/clk/CU, ds_write_b32 64 B/clk/CU, harmonic mean, "
+                                          "2.4 GHz); SQ counters in profiles/r02_pmc_sq_bp.json"},
+                     "roofline_hbm": {"bound": "hbm", "achieved_if_streamed": bach, "peak": HBM_PEAK_GBS,
+                                      "unit": "GB/s", "algorithmic_bytes_per_codeword_iteration": bbytes,
+                                      "traffic": hbm_meas,
+                                      "traffic_unit": "measured HBM bytes per codeword-iteration (PMC, "
+                                                      f"profiles/{bp_tfile})",
+                                      "note": "SURVEY.md 8(d)'s figure assumes the messages stream through HBM; "
+                                              "here they stay in LDS, so this bound does not bind (no frac)"}}
 
     if not args.no_sc:
-        out["sc"] = sc_bench(args, d, comm, args.cpu_seconds / 2 if d.world == 1 else 0)
+        out["sc"] = sc_bench(args, d, comm, 0.4 * args.cpu_seconds if cpu_on else 0, procs)
 
     if not args.no_concat:
         out["concat"] = concat_bench(args, d)
 
-    if d.rank == 0 and d.world == 1 and args.cpu_seconds > 0:
-        out["cpu_baseline"] = amp_cpu_baseline(st, args, args.cpu_seconds)
+    if cpu_on:
+        out["cpu_baseline"] = amp_cpu_baseline(st, args, args.cpu_seconds, procs)
         if not args.no_bp:
-            out["bp"]["cpu_baseline"] = bp_cpu_baseline(bst, args.cpu_seconds / 3)
+            out["bp"]["cpu_baseline"] = bp_cpu_baseline(bst, 0.4 * args.cpu_seconds, procs)
     if d.rank == 0:
         print(json.dumps(out), flush=True)
     if comm is not None:

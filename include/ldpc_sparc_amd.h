@@ -45,6 +45,7 @@ enum sg_precision { SG_F64 = 0, SG_F32 = 1 };
 const char *sg_last_error(void);
 const char *sg_version(void);
 int sg_device_count(int *count);
+int sg_device_cu_count(int *cus); /* compute units of the current device */
 int sg_set_device(int device);
 int sg_get_stream(void **stream);           /* library stream of the current device */
 int sg_malloc(void **dptr, size_t bytes);
@@ -136,6 +137,7 @@ typedef struct sg_comm sg_comm;
 int sg_comm_unique_id(void *id_out /* 128 bytes */);
 int sg_comm_init(int nranks, int rank, const void *id, sg_comm **out);
 int sg_comm_allreduce_sum_i64(sg_comm *c, int64_t *d_buf, size_t count, void *stream);
+int sg_comm_info(sg_comm *c, int *nranks, int *device); /* ranks and device as RCCL sees them */
 int sg_comm_destroy(sg_comm *c);
 
 /* ------------------------------------------------------------------- LDPC */
@@ -270,6 +272,11 @@ int sg_amp_plan_info(const sg_amp_plan *p, int *w, int *nT, int *Mr, int *Mc, in
  * (amp_cw.hip), 3 block (amp_block.hip).  Reads SG_AMP_ENGINE like the
  * decoder; returns the engine or a negative error code. */
 int sg_amp_plan_engine(const sg_amp_plan *p, int B);
+/* What the last decode through this plan ran: *engine as sg_amp_plan_engine
+ * (-1 before any decode), *handover_iter the first iteration the per-codeword
+ * engine left to the staged engine (-1: no hand-over), *on_companion 1 when
+ * the decode ran on the P = 16384 companion plan (may be NULL). */
+int sg_amp_last_decode(const sg_amp_plan *p, int *engine, int *handover_iter, int *on_companion);
 
 /* Batched AMP decode (sparc.py:883-999, one call per codeword in the
  * reference): y[B][n] received words sharing the plan's design; true_idx

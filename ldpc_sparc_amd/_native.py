@@ -38,6 +38,7 @@ SIGNATURES = [
     ("sg_last_error", ct.c_char_p, []),
     ("sg_version", ct.c_char_p, []),
     ("sg_device_count", ct.c_int, [ct.POINTER(ct.c_int)]),
+    ("sg_device_cu_count", ct.c_int, [ct.POINTER(ct.c_int)]),
     ("sg_set_device", ct.c_int, [ct.c_int]),
     ("sg_get_stream", ct.c_int, [ct.POINTER(vp)]),
     ("sg_malloc", ct.c_int, [ct.POINTER(vp), ct.c_size_t]),
@@ -69,6 +70,7 @@ SIGNATURES = [
     ("sg_amp_plan_destroy", ct.c_int, [vp]),
     ("sg_amp_plan_info", ct.c_int, [vp] + [ct.POINTER(ct.c_int)] * 6),
     ("sg_amp_plan_engine", ct.c_int, [vp, ct.c_int]),
+    ("sg_amp_last_decode", ct.c_int, [vp, ct.POINTER(ct.c_int), ct.POINTER(ct.c_int), ct.POINTER(ct.c_int)]),
     ("sg_amp_decode", ct.c_int, [vp, vp, ct.c_int, vp, ct.c_double, ct.c_int, ct.c_double, ct.c_int,
                                  vp, vp, vp, vp]),
     ("sg_amp_decode_device", ct.c_int, [vp, vp, ct.c_int, vp, ct.c_double, ct.c_int, ct.c_double,
@@ -86,6 +88,7 @@ SIGNATURES = [
     ("sg_comm_unique_id", ct.c_int, [vp]),
     ("sg_comm_init", ct.c_int, [ct.c_int, ct.c_int, vp, ct.POINTER(vp)]),
     ("sg_comm_allreduce_sum_i64", ct.c_int, [vp, vp, ct.c_size_t, vp]),
+    ("sg_comm_info", ct.c_int, [vp, ct.POINTER(ct.c_int), ct.POINTER(ct.c_int)]),
     ("sg_comm_destroy", ct.c_int, [vp]),
     ("sg_dense_plan_create", ct.c_int, [vp, ct.c_int, ct.c_int, ct.c_int, ct.c_double, ct.c_int,
                                         ct.POINTER(vp)]),
@@ -162,6 +165,12 @@ def check(rc):
 def device_count():
     n = ct.c_int(0)
     check(lib().sg_device_count(ct.byref(n)))
+    return n.value
+
+
+def cu_count():
+    n = ct.c_int(0)
+    check(lib().sg_device_cu_count(ct.byref(n)))
     return n.value
 
 
@@ -297,7 +306,22 @@ class Comm:
     def allreduce_sum_i64(self, dbuf, count, stream=None):
         check(lib().sg_comm_allreduce_sum_i64(self.h, dbuf.ptr, int(count), stream))
 
+    def info(self):
+        """(ranks, device) of this communicator as RCCL reports them."""
+        n, dev = ct.c_int(0), ct.c_int(-1)
+        check(lib().sg_comm_info(self.h, ct.byref(n), ct.byref(dev)))
+        return n.value, dev.value
+
     def destroy(self):
         if self.h is not None:
             lib().sg_comm_destroy(self.h)
             self.h = None
+
+
+def amp_last_decode(plan):
+    """What the last decode through `plan` ran: {"engine": 0 general / 1 staged /
+    2 per-codeword / 3 block, "handover_iter": first staged iteration after the
+    per-codeword engine (-1: none), "companion": ran on the P = 16384 plan}."""
+    e, h, c = ct.c_int(-1), ct.c_int(-1), ct.c_int(0)
+    check(lib().sg_amp_last_decode(plan, ct.byref(e), ct.byref(h), ct.byref(c)))
+    return {"engine": e.value, "handover_iter": h.value, "companion": bool(c.value)}

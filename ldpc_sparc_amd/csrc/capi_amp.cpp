@@ -15,6 +15,11 @@ using cd = std::complex<double>;
 
 struct sg_amp_plan {
     int precision = SG_F32;
+    // what the last decode through this handle ran (sg_amp_last_decode): the
+    // sub-plan (itself or the companion), its first engine, and the iteration
+    // at which the per-codeword engine handed over to the staged one (-1: none)
+    sg_amp_plan *last_ran = nullptr;
+    int last_engine = -1, last_handover = -1;
     int device = 0;
     int ndim = 0, L = 0, M = 0, LM = 0, n = 0, Lr = 1, Lc = 1, Mr = 0, Mc = 0, nT = 0;
     int w = 0, N2 = 0, P = 0, Q = 0, log2P = 0, log2Q = 0, npairs = 0;
@@ -241,6 +246,18 @@ static AmpTables<T> tables(const sg_amp_plan *p) {
     return tb;
 }
 
+// Phase ablation for timing studies (tools/ablate3.sh): compiled only into a
+// diagnostic build (make DIAG=1), because the results are wrong when a phase
+// is skipped.  The product library ignores SG_AMP_SKIP.
+static int diag_skip() {
+#ifdef SG_DIAG
+    const char *sk = std::getenv("SG_AMP_SKIP");
+    return sk ? std::atoi(sk) : 0;
+#else
+    return 0;
+#endif
+}
+
 static BlkTables btables(const sg_amp_plan *p) {
     BlkTables tb;
     tb.nT = p->nT; tb.L = p->L; tb.M = p->M; tb.LM = p->LM; tb.n = p->n; tb.Lr = p->Lr; tb.Lc = p->Lc;
@@ -249,8 +266,7 @@ static BlkTables btables(const sg_amp_plan *p) {
     tb.pos2 = p->b_pos2; tb.oab = p->b_oab; tb.oc = (const cx<float> *)p->b_oc;
     tb.ngs = p->b_ngs; tb.gptr = p->b_gptr; tb.grow = p->b_grow; tb.gloc = p->b_gloc; tb.gi = p->b_gi; tb.gc = (const cx<float> *)p->b_gc;
     tb.stw = (const cx<float> *)p->b_stw;
-    const char *sk = std::getenv("SG_AMP_SKIP");  // timing ablation only: results are wrong when set
-    tb.skip = sk ? std::atoi(sk) : 0;
+    tb.skip = diag_skip();
     return tb;
 }
 
@@ -601,8 +617,7 @@ static RegTables<T> rtables(const sg_amp_plan *p) {
     tb.twHi = (const cx<T> *)p->twHi; tb.twLo = (const cx<T> *)p->twLo;
     tb.stw = (const cx<T> *)p->r_stw; tb.twa = (const cx<T> *)p->r_twa; tb.twb = (const cx<T> *)p->r_twb;
     tb.nB = p->nB;
-    const char *sk = std::getenv("SG_AMP_SKIP");  // timing ablation only: results are wrong when set
-    tb.skip = sk ? std::atoi(sk) : 0;
+    tb.skip = diag_skip();
     return tb;
 }
 
@@ -940,10 +955,13 @@ static int decode_regular(sg_amp_plan *p, const void *d_y, int B, const int32_t 
     SG_TRY(reg_launch_init(B, p->Lc, t_max, p->ws_nmse, p->ws_active, p->ws_tfinal, s));
     std::vector<int32_t> act(B);
     bool cw = std::is_same<T, float>::value && use_cw(p, B);
+    p->last_engine = cw ? 2 : 1;
+    p->last_handover = -1;
     const char *eng = std::getenv("SG_AMP_ENGINE");
     const bool cw_forced = eng && std::strcmp(eng, "cw") == 0;
     double handover = 0.5;  // active fraction below which the staged engine takes over
-    if (const char *h = std::getenv("SG_AMP_HANDOVER")) handover = atof(h);  // tuning knob
+    if (const char *h = std::getenv("SG_AMP_HANDOVER"))  // tuning knob, clamped to [0, 1]
+        handover = std::min(1.0, std::max(0.0, atof(h)));
     for (int t = 0; t < t_max - 1; ++t) {
         if constexpr (std::is_same<T, float>::value) {
             if (cw) SG_TRY(cw_launch_iter(ctables(p), bf, sc, pr, t, s));
@@ -967,7 +985,10 @@ static int decode_regular(sg_amp_plan *p, const void *d_y, int B, const int32_t 
             int na = 0;
             for (int b = 0; b < B; ++b) na += act[b] != 0;
             if (na == 0) break;
-            if (cw && !cw_forced && na < handover * B) cw = false;
+            if (cw && !cw_forced && na < handover * B) {
+                cw = false;
+                p->last_handover = t + 1;  // first iteration on the staged engine
+            }
         }
     }
     SG_HIP(hipMemsetAsync(p->ws_argmax, 0x7f, sizeof(int32_t) * B * p->L, s));
@@ -1004,6 +1025,8 @@ static int decode_impl(sg_amp_plan *p, const void *d_y, int B, const int32_t *d_
     std::vector<int32_t> act(B);
     const bool blk = p->block && sizeof(T) == 4;
     const BlkTables bt = blk ? btables(p) : BlkTables{};
+    p->last_engine = blk ? 3 : 0;
+    p->last_handover = -1;
     for (int t = 0; t < t_max - 1; ++t) {
         if constexpr (sizeof(T) == 4) {
             if (blk) {
@@ -1167,6 +1190,15 @@ int sg_amp_plan_engine(const sg_amp_plan *p, int B) {
     return p->block ? 3 : 0;
 }
 
+int sg_amp_last_decode(const sg_amp_plan *p, int *engine, int *handover_iter, int *on_companion) {
+    SG_CHECK_ARG(p && engine && handover_iter, "null argument");
+    const sg_amp_plan *r = p->last_ran ? p->last_ran : p;
+    *engine = r->last_engine;
+    *handover_iter = r->last_handover;
+    if (on_companion) *on_companion = (p->last_ran && p->last_ran != p) ? 1 : 0;
+    return SG_OK;
+}
+
 int sg_amp_plan_info(const sg_amp_plan *p, int *w, int *nT, int *Mr, int *Mc, int *P, int *Q) {
     SG_CHECK_ARG(p, "plan is NULL");
     if (w) *w = p->w;
@@ -1189,7 +1221,7 @@ int sg_amp_decode_device(sg_amp_plan *p, const void *d_y, int B, const int32_t *
     SG_CHECK_ARG(B >= 0, "negative batch");
     if (B == 0) return SG_OK;
     SG_CHECK_ARG(d_y, "d_y is NULL");
-    p = sg::decode_plan(p, B);
+    p = p->last_ran = sg::decode_plan(p, B);
     SG_TRY(ensure_device());
     SG_HIP(hipSetDevice(p->device));
     hipStream_t s = pick_stream(stream);
@@ -1207,7 +1239,7 @@ int sg_amp_decode(sg_amp_plan *p, const double *y, int B, const int32_t *true_id
     if (B == 0) return SG_OK;
     SG_CHECK_ARG(y && map_idx && t_final && nmse && psi, "null host buffer");
     SG_CHECK_ARG(t_max > 1, "t_max must be > 1 (sparc.py:168)");
-    p = sg::decode_plan(p, B);
+    p = p->last_ran = sg::decode_plan(p, B);
     SG_TRY(ensure_device());
     SG_HIP(hipSetDevice(p->device));
     hipStream_t s = lib_stream();
@@ -1277,7 +1309,7 @@ int sg_amp_encode_device(sg_amp_plan *p, const int32_t *d_idx, int B, void *d_x,
 int sg_amp_stage_profile(sg_amp_plan *p, int kernel, double *mean_cycles, int *nphases) {
     SG_CHECK_ARG(p && mean_cycles && nphases && (kernel == 0 || kernel == 1), "bad argument");
     *nphases = 0;
-    if (!p->tprof && p->alt) p = p->alt;  // a small batch ran on the companion plan
+    if (p->last_ran) p = p->last_ran;  // the sub-plan the last decode ran on (maybe the companion)
     if (!p->tprof) return SG_OK;
     std::vector<uint64_t> h(p->tprof_items * 8);
     SG_HIP(hipDeviceSynchronize());
@@ -1297,7 +1329,7 @@ int sg_amp_stage_profile(sg_amp_plan *p, int kernel, double *mean_cycles, int *n
 
 int sg_amp_stage_raw(sg_amp_plan *p, int kernel, uint64_t *out, size_t *items) {
     SG_CHECK_ARG(p && items && (kernel == 0 || kernel == 1), "bad argument");
-    if (!p->tprof && p->alt) p = p->alt;
+    if (p->last_ran) p = p->last_ran;
     *items = p->tprof ? p->tprof_items : 0;
     if (!p->tprof || !out) return SG_OK;
     const size_t ni = p->tprof_items;

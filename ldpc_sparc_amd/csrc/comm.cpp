@@ -59,6 +59,16 @@ int sg_comm_allreduce_sum_i64(sg_comm *c, int64_t *d_buf, size_t count, void *st
     return SG_OK;
 }
 
+// Number of ranks and this rank's device as RCCL sees them (ncclCommCount,
+// ncclCommCuDevice): bench.py reports the rank count RCCL saw, not the one
+// it asked for.
+int sg_comm_info(sg_comm *c, int *nranks, int *device) {
+    SG_CHECK_ARG(c && nranks && device, "null argument");
+    SG_NCCL(ncclCommCount(c->comm, nranks));
+    SG_NCCL(ncclCommCuDevice(c->comm, device));
+    return SG_OK;
+}
+
 int sg_comm_destroy(sg_comm *c) {
     if (!c) return SG_OK;
     if (c->comm) ncclCommDestroy(c->comm);

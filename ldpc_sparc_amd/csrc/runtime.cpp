@@ -135,6 +135,13 @@ int sg_device_count(int *count) {
     return SG_OK;
 }
 
+int sg_device_cu_count(int *cus) {
+    SG_CHECK_ARG(cus, "cus is NULL");
+    SG_TRY(sg::ensure_device());
+    *cus = sg::device_cu_count();
+    return SG_OK;
+}
+
 int sg_set_device(int device) {
     SG_TRY(ensure_device());
     SG_HIP(hipSetDevice(device));

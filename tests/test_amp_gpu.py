@@ -410,13 +410,63 @@ def test_auto_engine_handover_matches_staged(monkeypatch):
     op = sparc.DesignOperator(W, L, M, n, o0, o1)
     Y = op.apply(beta0.astype(np.float64), False) + rng.standard_normal((B, n))
     monkeypatch.delenv("SG_AMP_ENGINE", raising=False)
+    monkeypatch.delenv("SG_AMP_HANDOVER", raising=False)
     ma, ta, na, _ = sparc.amp_decode_batch(Y, op, 1.0, 25, true_idx=true, precision=_native.SG_F32)
     assert _native.lib().sg_amp_plan_engine(op.plan(_native.SG_F32), B) == 2
+    last = _native.amp_last_decode(op.plan(_native.SG_F32))
+    # the hand-over really happened, before the last codeword stopped
+    assert last["engine"] == 2 and not last["companion"]
+    assert 0 < last["handover_iter"] < int(ta.max()), (last, np.bincount(ta))
     monkeypatch.setenv("SG_AMP_ENGINE", "staged")
     ms, ts, ns, _ = sparc.amp_decode_batch(Y, op, 1.0, 25, true_idx=true, precision=_native.SG_F32)
     assert np.array_equal(ma, true) and np.array_equal(ms, true)
     assert np.all(np.abs(ta - ts) <= 1)
     np.testing.assert_allclose(na[:, :8], ns[:, :8], atol=1e-3)
+
+
+def _c2_batch(seed_design, seed_data, B, R):
+    W, L, M, n, o0, o1 = _c2_design(seed_design, R=R)
+    rng = np.random.default_rng(seed_data)
+    true = rng.integers(0, M, (B, L)).astype(np.int32)
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    beta0 = np.zeros((B, L * M))
+    beta0[np.arange(B)[:, None], np.arange(L) * M + true] = 1
+    Y = op.apply(beta0, False) + rng.standard_normal((B, n))
+    return W, L, M, n, o0, o1, op, true, Y
+
+
+@pytest.mark.parametrize("R", [1.5, 1.3])
+def test_shipped_c2_batch_vs_oracle(monkeypatch, R):
+    """The path bench.py times: C2 (L=1024, M=512, n=6144 at R=1.5 / 7089 at
+    R=1.3), B=256, the automatic engine choice (per-codeword engine, hand-over
+    to the staged engine once half the batch stopped), f32 -- against the CPU
+    restatement of sparc.py:883-999 (float128 softmax) on 16 codewords of the
+    batch.  f32 bar: t_final within 2 of the reference's; section
+    decisions identical on >= 99 % of the sections of every codeword (all of
+    them on codewords the reference decodes); NMSE per iteration within 1e-3
+    over the first 6 iterations."""
+    from oracle import cpu_pool
+    monkeypatch.delenv("SG_AMP_ENGINE", raising=False)
+    monkeypatch.delenv("SG_AMP_HANDOVER", raising=False)
+    B = 256
+    W, L, M, n, o0, o1, op, true, Y = _c2_batch(41, 7, B, R)
+    plan = op.plan(_native.SG_F32)
+    assert _native.lib().sg_amp_plan_engine(plan, B) == 2
+    mi, tf, nm, _ = sparc.amp_decode_batch(Y, op, 1.0, 25, true_idx=true, precision=_native.SG_F32)
+    assert _native.amp_last_decode(plan)["engine"] == 2
+    pick = list(range(0, B, B // 16))
+    res, _ = cpu_pool.amp_decode(cpu_pool.host_cores(8), W, L, M, n, o0, o1, Y, true, 25, order=pick)
+    assert sorted(res) == pick
+    for b in pick:
+        cm, ct_, cn = res[b]
+        assert abs(int(tf[b]) - ct_) <= 2, (b, tf[b], ct_)
+        same = np.mean(mi[b] == cm)
+        if np.array_equal(cm, true[b]):
+            assert same == 1.0, (b, same)
+        assert same >= 0.99, (b, same)
+        np.testing.assert_allclose(nm[b, :6, 0], cn[:6], atol=1e-3)
+    if R == 1.3:  # decodable rate: most codewords decode, on both sides
+        assert np.mean([np.array_equal(res[b][0], true[b]) for b in pick]) >= 0.75
 
 
 @pytest.mark.gpu

@@ -33,6 +33,15 @@ for k in sorted(set(fetch) | set(write)):
     per[k] = {"dispatches": d, "read_bytes_per_dispatch": 2.0 * fetch.get(k, 0.0) * 1024 / d,
               "write_bytes_per_dispatch": write.get(k, 0.0) * 1024 / d}
 out = {"kernels": per, "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes; FETCH x2 (gfx950)"}
+rf = bench.get("roofline", {})
+cwk = next((n for n in per if n.startswith("cw_iter")), None)
+if cwk and rf.get("codeword_iterations_per_launch"):
+    b = per[cwk]["read_bytes_per_dispatch"] + per[cwk]["write_bytes_per_dispatch"]
+    out["amp"] = {"kernel": cwk, "hbm_bytes_per_launch": b,
+                  "hbm_bytes_per_codeword_iteration": b / rf["codeword_iterations_per_launch"],
+                  "codeword_iterations_per_launch": rf["codeword_iterations_per_launch"],
+                  "algorithmic_bytes_per_codeword_iteration": bench.get("roofline_hbm", {}).get(
+                      "algorithmic_bytes_per_codeword_iteration")}
 bp = bench.get("bp")
 if bp:
     units = bp["batch_per_gpu"] * bp["avg_executed_iterations"]
@@ -40,7 +49,8 @@ if bp:
     if k:
         b = per[k]["read_bytes_per_dispatch"] + per[k]["write_bytes_per_dispatch"]
         out["bp"] = {"kernel": k, "hbm_bytes_per_codeword_iteration": b / units,
-                     "algorithmic_bytes_per_codeword_iteration": bp["roofline"]["algorithmic_bytes_per_codeword_iteration"],
+                     "algorithmic_bytes_per_codeword_iteration": bp.get("roofline_hbm", bp["roofline"]).get(
+                         "algorithmic_bytes_per_codeword_iteration"),
                      "codeword_iterations_per_dispatch": units}
 sc = bench.get("sc")
 if sc:

@@ -1,0 +1,46 @@
+"""Per-kernel SQ counter summary of tools/pmc_sq_bench.sh's two passes:
+waits, VALU and LDS issue as fractions of wave cycles, LDS bank-conflict
+cycles as a fraction of LDS-array cycles (SQ_LDS_BANK_CONFLICT /
+SQ_LDS_IDX_ACTIVE, MI355X_MICROARCH.md LDS section).
+
+usage: python tools/pmc_sq_bench.py pass1.csv pass2.csv out.json"""
+import collections
+import csv
+import json
+import sys
+
+
+def load(path):
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    n = collections.defaultdict(set)
+    for r in csv.DictReader(open(path)):
+        name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("sg::", "")
+        agg[name][r["Counter_Name"]] += float(r["Counter_Value"])
+        n[name].add(r["Dispatch_Id"])
+    return agg, n
+
+
+a1, n1 = load(sys.argv[1])
+a2, _ = load(sys.argv[2])
+out = {}
+for k in sorted(a1):
+    if not (k.startswith("cw_iter") or k.startswith("bp_flood_kernel")):
+        continue
+    c = dict(a1[k])
+    c.update(a2.get(k, {}))
+    wc = c.get("SQ_WAVE_CYCLES", 0.0) or 1.0
+    lds = c.get("SQ_LDS_IDX_ACTIVE", 0.0) or 1.0
+    out[k] = {"dispatches": len(n1[k]), "counters": c,
+              "wait_any_frac": c.get("SQ_WAIT_ANY", 0) / wc,
+              "active_any_frac": c.get("SQ_ACTIVE_INST_ANY", 0) / wc,
+              "valu_active_frac": c.get("SQ_ACTIVE_INST_VALU", 0) / wc,
+              "lds_active_frac": c.get("SQ_ACTIVE_INST_LDS", 0) / wc,
+              "wait_inst_lds_frac": c.get("SQ_WAIT_INST_LDS", 0) / wc,
+              "lds_bank_conflict_frac": c.get("SQ_LDS_BANK_CONFLICT", 0) / lds,
+              "lds_insts_per_wave": c.get("SQ_INSTS_LDS", 0) / max(c.get("SQ_WAVES", 1), 1),
+              "valu_insts_per_wave": c.get("SQ_INSTS_VALU", 0) / max(c.get("SQ_WAVES", 1), 1)}
+res = {"kernels": out, "method": "rocprofv3 --pmc, two passes of 8 SQ counters over "
+                                  "bench.py --cpu-seconds 0 --no-concat --no-r13 --no-sc --steps 2 --warmup 1 "
+                                  "--bp-steps 3; fractions of SQ_WAVE_CYCLES (summed over waves)"}
+json.dump(res, open(sys.argv[3], "w"), indent=1)
+print(json.dumps({k: {kk: v for kk, v in d.items() if kk != "counters"} for k, d in out.items()}, indent=1))
