@@ -718,7 +718,7 @@ def main():
                                   "note": "the messages never leave LDS: 16 Nmsg bytes of f32 message reads and "
                                           "writes per codeword-iteration against the LDS peak for that mix "
                                           "(ds_read_b32 128 B/clk/CU, ds_write_b32 64 B/clk/CU, harmonic mean, "
-                                          "2.4 GHz); SQ counters in profiles/r02_pmc_sq_bp.json"},
+                                          "2.4 GHz); SQ counters in profiles/r02_pmc_sq_bench.json"},
                      "roofline_hbm": {"bound": "hbm", "achieved_if_streamed": bach, "peak": HBM_PEAK_GBS,
                                       "unit": "GB/s", "algorithmic_bytes_per_codeword_iteration": bbytes,
                                       "traffic": hbm_meas,
