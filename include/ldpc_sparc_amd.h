@@ -172,6 +172,11 @@ int sg_ldpc_decode_device(sg_graph *g, int dectype, int precision, const void *d
 int sg_ldpc_count_errors_device(sg_graph *g, int precision, const void *d_app, const uint8_t *d_x,
                                 const int32_t *d_it, int B, int k, int64_t *d_counts,
                                 void *stream);
+/* Bit errors (hard decision app < 0 against d_x, over all Nv bits) of each
+ * codeword: d_bit_errors[B].  The per-codeword form lets a campaign stop at
+ * the codeword where the frame-error count is reached (ldpc_awgn.py:86-105). */
+int sg_ldpc_codeword_errors_device(sg_graph *g, int precision, const void *d_app, const uint8_t *d_x, int B,
+                                   int32_t *d_bit_errors, void *stream);
 
 /* ------------------------------------------- device encoder and channel */
 /* Throughput-mode generation, keyed by Philox4x32-10

@@ -59,6 +59,7 @@ SIGNATURES = [
     ("sg_ldpc_decode", ct.c_int, [vp, ct.c_int, ct.c_int, vp, ct.c_int, ct.c_int, ct.c_double, vp, vp]),
     ("sg_ldpc_decode_device", ct.c_int,
      [vp, ct.c_int, ct.c_int, vp, ct.c_int, ct.c_int, ct.c_double, vp, vp, vp]),
+    ("sg_ldpc_codeword_errors_device", ct.c_int, [vp, ct.c_int, vp, vp, ct.c_int, vp, vp]),
     ("sg_ldpc_count_errors_device", ct.c_int,
      [vp, ct.c_int, vp, vp, vp, ct.c_int, ct.c_int, vp, vp]),
     ("sumprod", ct.c_int, [dp, lp, lp, lp, ct.c_int, ct.c_int, ct.c_int, dp, ct.c_int]),

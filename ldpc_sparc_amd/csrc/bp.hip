@@ -267,7 +267,8 @@ template int bp_launch<double>(const BpArgs<double> &, int, int, hipStream_t);
 template <typename T>
 __global__ __launch_bounds__(256) void bp_count_kernel(const T *__restrict__ app, const uint8_t *__restrict__ x,
                                                        const int32_t *__restrict__ its, int nv, int k,
-                                                       unsigned long long *__restrict__ counts) {
+                                                       unsigned long long *__restrict__ counts,
+                                                       int32_t *__restrict__ per_cw) {
     __shared__ int red[2][4];
     const int cw = blockIdx.x;
     int e_all = 0, e_k = 0;
@@ -287,24 +288,29 @@ __global__ __launch_bounds__(256) void bp_count_kernel(const T *__restrict__ app
     if (threadIdx.x == 0) {
         int ta = 0, tk = 0;
         for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { ta += red[0][w]; tk += red[1][w]; }
-        atomicAdd(&counts[0], (unsigned long long)ta);
-        atomicAdd(&counts[1], (unsigned long long)(ta > 0 ? 1 : 0));
-        atomicAdd(&counts[2], (unsigned long long)tk);
-        atomicAdd(&counts[3], (unsigned long long)its[cw]);
+        if (per_cw) per_cw[cw] = ta;  // bit errors of this codeword over all nv bits
+        if (counts) {
+            atomicAdd(&counts[0], (unsigned long long)ta);
+            atomicAdd(&counts[1], (unsigned long long)(ta > 0 ? 1 : 0));
+            atomicAdd(&counts[2], (unsigned long long)tk);
+            atomicAdd(&counts[3], (unsigned long long)its[cw]);
+        }
     }
 }
 
 template <typename T>
 int bp_count_launch(const T *app, const uint8_t *x, const int32_t *its, int B, int nv, int k,
-                    int64_t *counts, hipStream_t s) {
+                    int64_t *counts, hipStream_t s, int32_t *per_cw) {
     if (B <= 0) return SG_OK;
     hipLaunchKernelGGL(bp_count_kernel<T>, dim3(B), dim3(256), 0, s, app, x, its, nv, k,
-                       reinterpret_cast<unsigned long long *>(counts));
+                       reinterpret_cast<unsigned long long *>(counts), per_cw);
     SG_HIP(hipGetLastError());
     return SG_OK;
 }
-template int bp_count_launch<float>(const float *, const uint8_t *, const int32_t *, int, int, int, int64_t *, hipStream_t);
-template int bp_count_launch<double>(const double *, const uint8_t *, const int32_t *, int, int, int, int64_t *, hipStream_t);
+template int bp_count_launch<float>(const float *, const uint8_t *, const int32_t *, int, int, int, int64_t *, hipStream_t,
+                                    int32_t *);
+template int bp_count_launch<double>(const double *, const uint8_t *, const int32_t *, int, int, int, int64_t *,
+                                     hipStream_t, int32_t *);
 
 // ---------------------------------------------------------------- scalar helpers
 // Device evaluation of the reference's exported Lxor / Lxfb utilities.

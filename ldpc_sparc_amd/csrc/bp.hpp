@@ -27,7 +27,7 @@ template <typename T>
 int bp_launch(const BpArgs<T> &a, int dectype, int max_cdeg, hipStream_t s);
 template <typename T>
 int bp_count_launch(const T *app, const uint8_t *x, const int32_t *its, int B, int nv, int k,
-                    int64_t *counts, hipStream_t s);
+                    int64_t *counts, hipStream_t s, int32_t *per_cw = nullptr);
 int lxfb_launch(double *dL, int dc, int corr, double *dagg, hipStream_t s);
 
 }  // namespace sg

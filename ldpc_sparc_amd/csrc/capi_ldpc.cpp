@@ -262,6 +262,16 @@ int sg_ldpc_count_errors_device(sg_graph *g, int precision, const void *d_app, c
     return bp_count_launch<float>((const float *)d_app, d_x, d_it, B, g->nv, k, d_counts, s);
 }
 
+int sg_ldpc_codeword_errors_device(sg_graph *g, int precision, const void *d_app, const uint8_t *d_x, int B,
+                                   int32_t *d_bit_errors, void *stream) {
+    SG_CHECK_ARG(g && d_app && d_x && d_bit_errors, "null argument");
+    SG_TRY(ensure_device());
+    hipStream_t s = pick_stream(stream);
+    if (precision == SG_F64)
+        return bp_count_launch<double>((const double *)d_app, d_x, nullptr, B, g->nv, g->nv, nullptr, s, d_bit_errors);
+    return bp_count_launch<float>((const float *)d_app, d_x, nullptr, B, g->nv, g->nv, nullptr, s, d_bit_errors);
+}
+
 int sumprod(double *ch, long *vdeg, long *cdeg, long *intrlv, int Nv, int Nc, int Nmsg, double *app,
             int max_itcount) {
     return shim_decode(SG_SUMPROD, ch, vdeg, cdeg, intrlv, Nv, Nc, Nmsg, app, 0.0, max_itcount);

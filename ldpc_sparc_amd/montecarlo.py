@@ -65,21 +65,47 @@ def _ckpt_path(checkpoint_dir, tag, point):
     return os.path.join(checkpoint_dir, f"{tag}_pt{point}.json")
 
 
+def _first_reaching(cum, need):
+    """Index of the first entry of the running count `cum` that reaches
+    `need`, or None."""
+    hit = np.nonzero(cum >= need)[0]
+    return int(hit[0]) if hit.size else None
+
+
 def run_point(trial, point, *, block, blocks_per_round, rank, world, agg, min_errors=None, max_units=None,
-              checkpoint_dir=None, tag="campaign"):
+              checkpoint_dir=None, tag="campaign", params=None):
     """Run one point until `min_errors` frame errors or `max_units` units
     (globally).  trial(point, first_block, n_blocks, block) -> int64[NC]
-    counters of the blocks [first_block, first_block + n_blocks)."""
+    counters of the blocks [first_block, first_block + n_blocks).
+
+    A trial with `per_unit = True` returns int64[n_blocks * block, NC] (one
+    row per codeword, in block order) instead; the round's rows of every rank
+    are then combined by the same single all-reduce (each rank fills its own
+    rows of a zero matrix), and the point stops exactly at the codeword where
+    the frame-error count reaches `min_errors` or the unit count reaches
+    `max_units`, in block order -- the stopping rule of ldpc_awgn.sim
+    (ldpc_awgn.py:86-105), whatever the number of ranks.
+
+    `params` (campaign parameters) is stored in the checkpoint; resuming with
+    different parameters raises ValueError instead of adding up counts of
+    different experiments."""
     total = np.zeros(NC, dtype=np.int64)
     next_block = 0
+    done = False
+    params = dict(params or {}, block=int(block))
     if checkpoint_dir:
         path = _ckpt_path(checkpoint_dir, tag, point)
         if os.path.exists(path):
             with open(path) as f:
                 st = json.load(f)
+            if st.get("params") != json.loads(json.dumps(params)):
+                raise ValueError(f"checkpoint {path} was written with parameters {st.get('params')}, "
+                                 f"not {params}: use another checkpoint_dir or tag")
             total = np.array(st["counts"], dtype=np.int64)
             next_block = int(st["next_block"])
-    while True:
+            done = bool(st.get("done", False))
+    per_unit = getattr(trial, "per_unit", False)
+    while not done:
         if min_errors is not None and total[2] >= min_errors:
             break
         if max_units is not None and total[0] >= max_units:
@@ -88,14 +114,29 @@ def run_point(trial, point, *, block, blocks_per_round, rank, world, agg, min_er
         if max_units is not None:
             nb = min(nb, -(-(max_units - int(total[0])) // block))
         a, b = shard_range(nb, rank, world)
-        local = trial(point, next_block + a, b - a, block) if b > a else np.zeros(NC, dtype=np.int64)
-        total = total + agg.allreduce(local)  # the campaign's one collective per round
+        if per_unit:
+            rows = np.zeros((nb * block, NC), dtype=np.int64)
+            if b > a:
+                rows[a * block:b * block] = trial(point, next_block + a, b - a, block)
+            rows = agg.allreduce(rows.ravel()).reshape(nb * block, NC)  # the one collective per round
+            cut = len(rows)
+            if min_errors is not None:
+                k = _first_reaching(total[2] + np.cumsum(rows[:, 2]), min_errors)
+                if k is not None:
+                    cut, done = min(cut, k + 1), True
+            if max_units is not None and total[0] + cut >= max_units:
+                cut, done = max_units - int(total[0]), True
+            total = total + rows[:cut].sum(axis=0)
+        else:
+            local = trial(point, next_block + a, b - a, block) if b > a else np.zeros(NC, dtype=np.int64)
+            total = total + agg.allreduce(local)  # the campaign's one collective per round
         next_block += nb
         if checkpoint_dir and rank == 0:
             os.makedirs(checkpoint_dir, exist_ok=True)
             tmp = _ckpt_path(checkpoint_dir, tag, point) + ".tmp"
             with open(tmp, "w") as f:
-                json.dump({"counts": total.tolist(), "next_block": next_block}, f)
+                json.dump({"counts": total.tolist(), "next_block": next_block, "done": done,
+                           "params": params}, f)
             os.replace(tmp, _ckpt_path(checkpoint_dir, tag, point))
         if min_errors is None and max_units is None:
             break
@@ -110,8 +151,10 @@ class LdpcTrial:
     decoded in batches on the GPU; counts over all N bits as the reference
     does (ldpc_awgn.py:97-104).  aux0 = sum of decode iteration counts."""
 
-    def __init__(self, c, snrs, dectype="sumprod2", max_it=200, corr=0.7, precision="f32", seed=0, rng="host"):
+    def __init__(self, c, snrs, dectype="sumprod2", max_it=200, corr=0.7, precision="f32", seed=0, rng="host",
+                 per_unit=False):
         self.c, self.snrs, self.dectype = c, list(snrs), dectype
+        self.per_unit = bool(per_unit)  # per-codeword counter rows (exact stopping rule, run_point)
         self.max_it, self.corr, self.seed = int(max_it), float(corr), int(seed)
         self.prec = {"f64": _native.SG_F64, "f32": _native.SG_F32}[precision]
         if rng not in ("host", "device"):
@@ -164,10 +207,17 @@ class LdpcTrial:
         g = c._device_graph()
         d_app = _native.DeviceBuffer(B * c.N * np.dtype(dt).itemsize)
         d_it = _native.DeviceBuffer(B * 4)
-        d_cnt = _native.DeviceBuffer(32)
-        d_cnt.zero()
         _native.check(lib.sg_ldpc_decode_device(g, _native.DECTYPES[self.dectype], self.prec, d_ch.ptr, B,
                                                 self.max_it, self.corr, d_app.ptr, d_it.ptr, None))
+        if self.per_unit:  # one row per codeword: [1, bit errors, frame error, iterations, 0]
+            d_be = _native.DeviceBuffer(B * 4)
+            _native.check(lib.sg_ldpc_codeword_errors_device(g, self.prec, d_app.ptr, d_x.ptr, B, d_be.ptr, None))
+            _native.synchronize()
+            be = d_be.download(np.zeros(B, np.int32)).astype(np.int64)
+            it = d_it.download(np.zeros(B, np.int32)).astype(np.int64)
+            return np.stack([np.ones(B, np.int64), be, (be > 0).astype(np.int64), it, np.zeros(B, np.int64)], 1)
+        d_cnt = _native.DeviceBuffer(32)
+        d_cnt.zero()
         _native.check(lib.sg_ldpc_count_errors_device(g, self.prec, d_app.ptr, d_x.ptr, d_it.ptr, B, c.K,
                                                       d_cnt.ptr, None))
         _native.synchronize()
@@ -274,7 +324,10 @@ def concat_ber_sweep(L, M, n, P, L_unprotected, mults, ebn0_db, *, codewords, bl
     for point, e in enumerate(ebn0_db):
         tot = run_point(trial, point, block=block, blocks_per_round=bpr, rank=rank, world=world, agg=agg,
                         min_errors=min_errors, max_units=codewords, checkpoint_dir=checkpoint_dir,
-                        tag=f"concat_L{L}_M{M}_n{n}")
+                        tag=f"concat_L{L}_M{M}_n{n}",
+                        params={"P": P, "L_unprotected": L_unprotected, "mults": mults, "ebn0_db": float(e),
+                                "seed": seed, "design_seed": design_seed, "t_max": t_max, "bp_its": bp_its,
+                                "precision": precision, "ldpc": list(ldpc), "codewords": codewords})
         out.append({"ebn0_db": float(e), "awgn_var": vars_[point], "codewords": int(tot[0]),
                     "ber": float(tot[1]) / (tot[0] * user_bits) if tot[0] else None,
                     "fer": float(tot[2]) / tot[0] if tot[0] else None,
@@ -291,12 +344,15 @@ def concat_ber_sweep(L, M, n, P, L_unprotected, mults, ebn0_db, *, codewords, bl
 def ldpc_awgn_campaign(standard, rate, z, ptype="A", *, rank=0, world=1, agg=None, N_MEASUREMENTS=24,
                        C_AWGN_OFFSET=1.0, P_STEP=100.0, MIN_ERRORS=100, MAX_BLOCKS=400000, block=256,
                        blocks_per_round=16, dectype="sumprod2", max_it=200, precision="f32", seed=0,
-                       results_file=None, checkpoint_dir=None):
+                       results_file=None, checkpoint_dir=None, trial=None):
     """The BER/FER campaign of ldpc_awgn.sim (ldpc_awgn.py:60-114) on the GPU(s):
-    same starting SNR, stopping rule and SNR-step heuristic; returns and (rank
-    0) appends the result tuples (standard, rate, z, ptype, SNR, nblocks,
+    same starting SNR, stopping rule (each point ends at the codeword whose
+    frame error is the MIN_ERRORS-th, or at MAX_BLOCKS codewords, counted in
+    block order whatever the rank count) and SNR-step heuristic; returns and
+    (rank 0) appends the result tuples (standard, rate, z, ptype, SNR, nblocks,
     nblockerrors, nblocks*K, nbiterrors, nit_total) -- the 11-field form that
-    results2csv.c parses (results2csv.c:47-48)."""
+    results2csv.c parses (results2csv.c:47-48).  `trial` replaces the GPU
+    trial (tests)."""
     from .ldpc import code
     Rv = {"1/2": .5, "2/3": 0.6667, "3/4": 0.75, "5/6": 0.83333}
     if rate not in Rv:
@@ -305,12 +361,14 @@ def ldpc_awgn_campaign(standard, rate, z, ptype="A", *, rank=0, world=1, agg=Non
     c = code(standard, rate, z, ptype)
     snr = 10.0 * np.log10(np.power(2, Rv[rate]) - 1.0) + C_AWGN_OFFSET
     res = []
-    trial = LdpcTrial(c, [], dectype, max_it, 0.7, precision, seed)
+    trial = trial or LdpcTrial(c, [], dectype, max_it, 0.7, precision, seed, per_unit=True)
     for point in range(N_MEASUREMENTS):
         trial.snrs.append(snr)
+        params = {"seed": seed, "dectype": dectype, "max_it": max_it, "precision": precision, "snr": float(snr),
+                  "min_errors": MIN_ERRORS, "max_blocks": MAX_BLOCKS}
         tot = run_point(trial, point, block=block, blocks_per_round=blocks_per_round, rank=rank, world=world,
                         agg=agg, min_errors=MIN_ERRORS, max_units=MAX_BLOCKS, checkpoint_dir=checkpoint_dir,
-                        tag=f"ldpc_{standard}_{rate.replace('/', '')}_{z}_{ptype}")
+                        tag=f"ldpc_{standard}_{rate.replace('/', '')}_{z}_{ptype}", params=params)
         nblocks = int(tot[0])
         out = (standard, rate, z, ptype, snr, nblocks, int(tot[2]), nblocks * c.K, int(tot[1]), int(tot[3]))
         res.append(out)

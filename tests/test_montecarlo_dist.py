@@ -39,6 +39,52 @@ def test_shard_range_partitions():
             assert max(b - a for a, b in parts) - min(b - a for a, b in parts) <= 1
 
 
+class FakeUnitTrial:
+    """Per-codeword counter rows [1, bit errors, frame error, iterations, 0]
+    in block order (stands in for LdpcTrial(per_unit=True))."""
+    per_unit = True
+
+    def __init__(self, snrs=()):
+        self.snrs = list(snrs)
+
+    def rows(self, point, b, block):
+        snr = self.snrs[point] if self.snrs else point
+        rng = np.random.default_rng([11, point, b])
+        fe = rng.binomial(1, 1.0 / (2.0 + abs(snr)), block)
+        be = fe * rng.integers(1, 9, block)
+        return np.stack([np.ones(block, np.int64), be, fe, rng.integers(0, 50, block), np.zeros(block, np.int64)],
+                        1).astype(np.int64)
+
+    def __call__(self, point, first_block, n_blocks, block):
+        return np.concatenate([self.rows(point, b, block) for b in range(first_block, first_block + n_blocks)])
+
+
+def sequential_sim(trial, min_errors, max_blocks, block, n_points, snr0, p_step):
+    """Restatement of ldpc_awgn.sim's loop (ldpc_awgn.py:84-114): codewords one
+    by one in block order, stop at the MIN_ERRORS-th frame error or at
+    MAX_BLOCKS, then SNR += sqrt(P_STEP / nblocks)."""
+    snr, out = snr0, []
+    for point in range(n_points):
+        trial.snrs.append(snr)
+        nbiterrors = nblockerrors = nblocks = nit = 0
+        b = 0
+        rows = trial.rows(point, b, block)
+        while nblockerrors < min_errors:
+            r = rows[nblocks - b * block]
+            nbiterrors += int(r[1])
+            nblockerrors += int(r[2])
+            nit += int(r[3])
+            nblocks += 1
+            if nblocks >= max_blocks:
+                break
+            if nblocks % block == 0:
+                b += 1
+                rows = trial.rows(point, b, block)
+        out.append((snr, nblocks, nblockerrors, nbiterrors, nit))
+        snr += np.sqrt(p_step / nblocks)
+    return out
+
+
 def _worker(rank, world, port, q, ckpt):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -50,7 +96,9 @@ def _worker(rank, world, port, q, ckpt):
         res.append(mc.run_point(fake_trial, pt, block=64, blocks_per_round=5, rank=rank, world=world, agg=agg,
                                 min_errors=200, max_units=5000, checkpoint_dir=ckpt).tolist())
     s = agg.allreduce(np.array([rank + 1, 10], dtype=np.int64)).tolist()
-    q.put((rank, res, s))
+    camp = mc.ldpc_awgn_campaign("802.11n", "1/2", 27, rank=rank, world=world, agg=agg, N_MEASUREMENTS=4,
+                                 MIN_ERRORS=37, MAX_BLOCKS=3000, block=32, blocks_per_round=3, trial=FakeUnitTrial())
+    q.put((rank, res, s, camp))
     dist.destroy_process_group()
 
 
@@ -73,6 +121,9 @@ def test_campaign_world2_equals_world1(tmp_path):
     out = _run(2)
     assert out[0][1] == single and out[1][1] == single  # every rank sees the global counts
     assert out[0][2] == [3, 20] and out[1][2] == [3, 20]
+    camp1 = mc.ldpc_awgn_campaign("802.11n", "1/2", 27, N_MEASUREMENTS=4, MIN_ERRORS=37, MAX_BLOCKS=3000,
+                                  block=32, blocks_per_round=3, trial=FakeUnitTrial())
+    assert out[0][3] == camp1 and out[1][3] == camp1  # the exact stopping rule does not depend on the ranks
     for r in single:
         assert r[2] >= 200 or r[0] >= 5000
 
@@ -88,6 +139,38 @@ def test_checkpoint_resume(tmp_path):
                          min_errors=200, max_units=None)
     assert first[2] >= 30
     assert resumed.tolist() == fresh.tolist()
+
+
+def test_exact_stopping_rule_matches_sequential_sim():
+    """ldpc_awgn_campaign stops every point at the same codeword as the
+    reference's sequential loop, so nblocks, the counts and the SNR sequence
+    agree (ldpc_awgn.py:84-114), whatever the round size."""
+    for bpr in (1, 3, 16):
+        camp = mc.ldpc_awgn_campaign("802.11n", "1/2", 27, N_MEASUREMENTS=5, MIN_ERRORS=25, MAX_BLOCKS=400,
+                                     block=16, blocks_per_round=bpr, trial=FakeUnitTrial())
+        snr0 = 10.0 * np.log10(2 ** 0.5 - 1.0) + 1.0
+        ref = sequential_sim(FakeUnitTrial(), 25, 400, 16, 5, snr0, 100.0)
+        for c, r in zip(camp, ref):
+            assert c[4] == r[0] and (c[5], c[6], c[8], c[9]) == r[1:], (bpr, c, r)
+
+
+def test_exact_stop_at_max_blocks():
+    t = FakeUnitTrial([100.0])  # ~1 % frame errors: MAX_BLOCKS ends the point
+    tot = mc.run_point(t, 0, block=16, blocks_per_round=4, rank=0, world=1, agg=mc.Aggregator(), min_errors=1000,
+                       max_units=50)
+    assert tot[0] == 50 and tot[2] == t(0, 0, 4, 16)[:50, 2].sum()
+
+
+def test_checkpoint_refuses_other_parameters(tmp_path):
+    d = str(tmp_path)
+    mc.run_point(fake_trial, 0, block=64, blocks_per_round=5, rank=0, world=1, agg=mc.Aggregator(), min_errors=30,
+                 checkpoint_dir=d, params={"seed": 1})
+    with pytest.raises(ValueError):
+        mc.run_point(fake_trial, 0, block=64, blocks_per_round=5, rank=0, world=1, agg=mc.Aggregator(),
+                     min_errors=60, checkpoint_dir=d, params={"seed": 2})
+    with pytest.raises(ValueError):  # another block size is another experiment too
+        mc.run_point(fake_trial, 0, block=32, blocks_per_round=5, rank=0, world=1, agg=mc.Aggregator(),
+                     min_errors=60, checkpoint_dir=d, params={"seed": 1})
 
 
 def test_results_csv_format():
