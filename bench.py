@@ -402,6 +402,60 @@ def bp_cpu_baseline(st, seconds, procs):
                                   "channel LLRs, over every codeword of the CPU sample"}}
 
 
+def bp_variant(args, d, std, rate, z, dectype, prec, ebn0, B, steps, max_it=50, cpu_seconds=0.0, procs=1):
+    """A BP line beside C3: another decoder / precision / code through the same
+    batched engine, with the GPU's decisions compared to the CPU restatement
+    (oracle/bp_oracle.c) on the same LLRs when cpu_seconds > 0."""
+    c = code(std, rate, z)
+    rng = np.random.default_rng(3000 + d.rank)
+    X = c.encode_batch(rng.integers(0, 2, (B, c.K)))
+    R = c.K / c.N
+    s2 = 1 / (2 * R * 10 ** (ebn0 / 10))
+    ch = 2 * ((1 - 2 * X) + np.sqrt(s2) * rng.standard_normal(X.shape)) / s2
+    g = c._device_graph()
+    dt = np.float32 if prec == _native.SG_F32 else np.float64
+    d_ch = _native.DeviceBuffer.from_array(ch.astype(dt))
+    d_app = _native.DeviceBuffer(B * c.N * np.dtype(dt).itemsize)
+    d_it = _native.DeviceBuffer(B * 4)
+    kind = _native.DECTYPES[dectype]
+    lib = _native.lib()
+
+    def step():
+        _native.check(lib.sg_ldpc_decode_device(g, kind, prec, d_ch.ptr, B, max_it, 0.7, d_app.ptr, d_it.ptr, None))
+
+    step()
+    _native.device_synchronize()
+    prof = _native.Profiler()
+    d.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    _native.device_synchronize()
+    el = d.max(time.perf_counter() - t0)
+    ph = prof.stop()
+    its = d_it.download(np.zeros(B, np.int32))
+    app = d_app.download(np.zeros((B, c.N), dt))
+    hard = (app < 0).astype(np.int64)
+    fe = int((hard[:, :c.K] != X[:, :c.K]).any(1).sum())
+    out = {"workload": f"{std} r{rate} z={z} (n={c.N}, max check degree {int(c.cdeg.max())}), {dectype}, "
+                       f"{'f32' if prec == _native.SG_F32 else 'f64'}, max {max_it} it, Eb/N0 {ebn0} dB, random codewords",
+           "value": d.world * B * steps / el, "unit": "codewords/s", "batch_per_gpu": B,
+           "avg_executed_iterations": float(np.where(its < max_it, its + 1, max_it).mean()),
+           "frame_errors": fe, "kernel_ms_per_launch": ph.get("bp_flood", (0.0, 1))[0] / max(ph.get("bp_flood", (0, 1))[1], 1)}
+    if cpu_seconds > 0:
+        from oracle import cpu_pool
+        capp, cit, done, cel = cpu_pool.bp_decode(procs, dectype, ch, c.vdeg, c.cdeg, c.intrlv, max_it, 0.7,
+                                                  deadline_s=cpu_seconds)
+        ch_ = (capp[done] < 0).astype(np.int64)
+        out["cpu_baseline"] = {"value": int(done.sum()) / cel, "unit": "codewords/s", "cores": procs, "kind": "port",
+                               "sample": f"{int(done.sum())} of the {B} codewords, oracle/bp_oracle.c on {procs} cores",
+                               "identical_codeword_decisions": float((ch_ == hard[done]).all(1).mean()),
+                               "identical_iteration_counts": float((cit[done] == its[done]).mean()),
+                               "cpu_fer": float((ch_[:, :c.K] != X[done][:, :c.K]).any(1).mean()),
+                               "gpu_fer": float((hard[done][:, :c.K] != X[done][:, :c.K]).any(1).mean())}
+    return out
+
+
 # ------------------------------------------------------------------ spatially coupled (C4)
 
 def sc_bench(args, d, comm, cpu_seconds, procs):
@@ -726,6 +780,12 @@ def main():
                                                       f"profiles/{bp_tfile})",
                                       "note": "SURVEY.md 8(d)'s figure assumes the messages stream through HBM; "
                                               "here they stay in LDS, so this bound does not bind (no frac)"}}
+
+    if not args.no_bp:
+        cs = 0.1 * args.cpu_seconds if cpu_on else 0.0
+        out["bp_variants"] = [
+            bp_variant(args, d, "802.11n", "1/2", 81, "sumprod2", _native.SG_F64, 2.0, 1024, 3, 50, cs, procs),
+            bp_variant(args, d, "802.11n", "5/6", 81, "minsum", _native.SG_F32, 3.5, 4096, 5, 50, cs, procs)]
 
     if not args.no_sc:
         out["sc"] = sc_bench(args, d, comm, 0.4 * args.cpu_seconds if cpu_on else 0, procs)

@@ -123,13 +123,76 @@ __device__ __forceinline__ bool check_update(T *__restrict__ msg, int c, int nc,
     return unsat;
 }
 
+// Register-lean check update for high check degrees and double precision:
+// no per-port register arrays (they spilled: T L[MAXDC], f[MAXDC], b[MAXDC]).
+// The message slots themselves hold what a second pass needs; sum-product
+// (Lxfb) keeps its backward values b[k+1] in an LDS scratch image laid out
+// like the messages (scr[k * nc + c]), so every access stays conflict-free.
+// Same arithmetic, in the same order, as check_update.
+template <typename T, int KIND>
+__device__ __forceinline__ bool check_update_lean(T *__restrict__ msg, T *__restrict__ scr, int c, int nc, int d,
+                                                  T factor) {
+    bool unsat = false;
+    if (KIND == SG_MINSUM) {
+        T m1 = T(INFINITY), m2 = T(INFINITY);
+        int i1 = -1;
+        unsigned sgn = 0u, sall = 0u;
+        for (int k = 0; k < d; ++k) {
+            const T x = msg[k * nc + c];
+            const T a = fabs(x);
+            const unsigned sb = signbit(x) ? 1u : 0u;
+            sgn |= sb << k;
+            sall ^= sb;
+            if (a < m1) { m2 = m1; m1 = a; i1 = k; }
+            else if (a < m2) { m2 = a; }
+        }
+        unsat = (sall != 0u) || !(m1 > T(0));
+        for (int k = 0; k < d; ++k) {
+            const T mag = (k == i1) ? m2 : m1;
+            const bool neg = (sall ^ ((sgn >> k) & 1u)) != 0u;
+            msg[k * nc + c] = (neg ? -mag : mag) * factor;
+        }
+    } else if (KIND == SG_SUMPROD2) {
+        // backward values b[k] = Lxor(b[k+1], L[k]); b[k+1] kept for port k
+        T b = msg[(d - 1) * nc + c];
+        for (int k = d - 2; k >= 0; --k) {
+            scr[(k + 1) * nc + c] = b;
+            b = lxor<T, true>(b, msg[k * nc + c]);
+        }
+        unsat = !(b > T(0));  // b[0], the aggregate
+        // forward values f[k] = Lxor(f[k-1], L[k]); port k gets Lxor(f[k-1], b[k+1])
+        T f = msg[c];
+        msg[c] = scr[nc + c];  // L[0] = b[1]
+        for (int k = 1; k < d - 1; ++k) {
+            const T Lk = msg[k * nc + c];
+            msg[k * nc + c] = lxor<T, true>(f, scr[(k + 1) * nc + c]);
+            f = lxor<T, true>(f, Lk);
+        }
+        msg[(d - 1) * nc + c] = f;  // L[d-1] = f[d-2]
+    } else {  // SG_SUMPROD: the slots hold tanh(L/2) between the passes
+        T prod = T(1);
+        for (int k = 0; k < d; ++k) {
+            const T t = tanh(msg[k * nc + c] / T(2));
+            msg[k * nc + c] = t;
+            prod *= t;
+        }
+        unsat = (T(2) * atanh(prod)) <= T(0);
+        for (int k = 0; k < d; ++k) msg[k * nc + c] = T(2) * atanh(prod / msg[k * nc + c]);
+    }
+    return unsat;
+}
+
+// Kernels that take the lean path: double precision, and check degrees above 8
+template <typename T, int MAXDC>
+constexpr bool bp_lean() { return sizeof(T) == 8 || MAXDC > 8; }
+
 // LDS image of one workgroup: the messages of its current codeword and --
 // loaded once per workgroup -- the graph tables as 16-bit indices, so the
 // per-iteration passes never leave LDS.  The channel LLRs and the app of the
 // thread's variables (v = tid + BP_THREADS j) stay in registers.
 template <typename T>
-size_t bp_lds_bytes(int slots, int nv, int nports, int nc) {
-    size_t b = sizeof(T) * (size_t)slots;
+size_t bp_lds_bytes(int slots, int nv, int nports, int nc, bool scratch = false) {
+    size_t b = sizeof(T) * (size_t)slots * (scratch ? 2 : 1);
     b += sizeof(uint16_t) * ((size_t)nports + nv + 1) + nc;
     return (b + 15) / 16 * 16;
 }
@@ -144,8 +207,12 @@ constexpr int bp_waves_per_simd() { return (sizeof(T) == 4 && KIND == SG_MINSUM)
 template <typename T, int KIND, int MAXDC, int VJ>
 __global__ __launch_bounds__(BP_THREADS, (bp_waves_per_simd<T, KIND>())) void bp_flood_kernel(BpArgs<T> a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr bool LEAN = bp_lean<T, MAXDC>();
+    constexpr bool SCR = LEAN && KIND == SG_SUMPROD2;
+    constexpr bool LEANV = LEAN || VJ > 4;  // variable pass without per-port register arrays
     T *msg = reinterpret_cast<T *>(smem);
-    uint16_t *ps = reinterpret_cast<uint16_t *>(msg + a.slots);  // variable port -> message slot
+    T *scr = msg + (SCR ? a.slots : 0);                         // Lxfb backward values (lean sumprod2)
+    uint16_t *ps = reinterpret_cast<uint16_t *>(msg + (SCR ? 2 : 1) * a.slots);  // variable port -> message slot
     uint16_t *vo = ps + a.nports;                                // variable-port offsets
     uint8_t *cd = reinterpret_cast<uint8_t *>(vo + a.nv + 1);    // check degrees
     const int tid = threadIdx.x;
@@ -173,26 +240,36 @@ __global__ __launch_bounds__(BP_THREADS, (bp_waves_per_simd<T, KIND>())) void bp
                 const int p0 = vo[v];
                 const int d = vo[v + 1] - p0;
                 T acc = chv[j];
-                int s[BP_MAXDV];
-                T m[BP_MAXDV];
+                if constexpr (LEANV) {  // second pass re-reads the slots instead of holding them
+                    for (int k = 0; k < d; ++k) acc += msg[ps[p0 + k]];
+                    for (int k = 0; k < d; ++k) {
+                        const int sl = ps[p0 + k];
+                        msg[sl] = acc - msg[sl];
+                    }
+                } else {
+                    int s[BP_MAXDV];
+                    T m[BP_MAXDV];
 #pragma unroll
-                for (int k = 0; k < BP_MAXDV; ++k)
-                    if (k < d) { s[k] = ps[p0 + k]; m[k] = msg[s[k]]; acc += m[k]; }
-                for (int k = BP_MAXDV; k < d; ++k) acc += msg[ps[p0 + k]];
+                    for (int k = 0; k < BP_MAXDV; ++k)
+                        if (k < d) { s[k] = ps[p0 + k]; m[k] = msg[s[k]]; acc += m[k]; }
+                    for (int k = BP_MAXDV; k < d; ++k) acc += msg[ps[p0 + k]];
 #pragma unroll
-                for (int k = 0; k < BP_MAXDV; ++k)
-                    if (k < d) msg[s[k]] = acc - m[k];
-                for (int k = BP_MAXDV; k < d; ++k) {
-                    const int sl = ps[p0 + k];
-                    msg[sl] = acc - msg[sl];
+                    for (int k = 0; k < BP_MAXDV; ++k)
+                        if (k < d) msg[s[k]] = acc - m[k];
+                    for (int k = BP_MAXDV; k < d; ++k) {
+                        const int sl = ps[p0 + k];
+                        msg[sl] = acc - msg[sl];
+                    }
                 }
                 apv[j] = acc;
             }
             __syncthreads();
             // ---- check pass (c_ldpc.c:183-194)
             int unsat = 0;
-            for (int c = tid; c < a.nc; c += BP_THREADS)
-                unsat |= check_update<T, KIND, MAXDC>(msg, c, a.nc, cd[c], a.factor) ? 1 : 0;
+            for (int c = tid; c < a.nc; c += BP_THREADS) {
+                if constexpr (LEAN) unsat |= check_update_lean<T, KIND>(msg, scr, c, a.nc, cd[c], a.factor) ? 1 : 0;
+                else unsat |= check_update<T, KIND, MAXDC>(msg, c, a.nc, cd[c], a.factor) ? 1 : 0;
+            }
             if (!__syncthreads_or(unsat)) break;  // c_ldpc.c:196-197
         }
         T *out = a.app + (size_t)cw * a.nv;
@@ -209,6 +286,12 @@ __global__ __launch_bounds__(BP_THREADS, (bp_waves_per_simd<T, KIND>())) void bp
 template <typename T, int KIND, int MAXDC, int VJ>
 static int launch_one(const BpArgs<T> &a, size_t lds, hipStream_t s) {
     auto kern = bp_flood_kernel<T, KIND, MAXDC, VJ>;
+    if (bp_lean<T, MAXDC>() && KIND == SG_SUMPROD2) {  // + the LDS scratch of the backward values
+        lds = bp_lds_bytes<T>(a.slots, a.nv, a.nports, a.nc, true);
+        if (lds > BP_MAX_LDS)
+            return fail(SG_ERR_UNSUPPORTED, "graph needs %zu B of LDS per codeword for sum-product (> %d B)", lds,
+                        BP_MAX_LDS);
+    }
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BP_THREADS, lds) != hipSuccess || per_cu < 1)
         per_cu = 1;
