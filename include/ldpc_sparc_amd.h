@@ -187,6 +187,11 @@ int sg_ldpc_codeword_errors_device(sg_graph *g, int precision, const void *d_app
 int sg_rng_bits_device(uint64_t seed, uint64_t stream_id, int B, int nbits, uint8_t *d_bits, void *stream);
 /* section indices from MSB-first bit groups (sparc.py:330-364): d_bits [B][L*logM] -> d_idx [B][L] */
 int sg_bits_to_sections_device(const uint8_t *d_bits, int B, int L, int logM, int32_t *d_idx, void *stream);
+/* The same with row strides: codeword b's bits at d_bits + b * bit_stride,
+ * its L indices at d_idx + b * idx_stride (a part of a longer message, e.g.
+ * the protected sections of a concatenated codeword, sparc_new.py:15-51). */
+int sg_bits_to_sections_strided_device(const uint8_t *d_bits, size_t bit_stride, int B, int L, int logM,
+                                       int32_t *d_idx, size_t idx_stride, void *stream);
 /* y = x + sigma N(0, 1) [B][n] (sparc_sim.py:179-204) */
 int sg_awgn_device(int precision, uint64_t seed, uint64_t stream_id, const void *d_x, int B, int n, double sigma,
                    void *d_y, void *stream);

@@ -112,6 +112,8 @@ SIGNATURES = [
     ("sg_amp_stage_raw", ct.c_int, [vp, ct.c_int, vp, vp]),
     # device encoder and channel
     ("sg_rng_bits_device", ct.c_int, [ct.c_uint64, ct.c_uint64, ct.c_int, ct.c_int, vp, vp]),
+    ("sg_bits_to_sections_strided_device", ct.c_int,
+     [vp, ct.c_size_t, ct.c_int, ct.c_int, ct.c_int, vp, ct.c_size_t, vp]),
     ("sg_bits_to_sections_device", ct.c_int, [vp, ct.c_int, ct.c_int, ct.c_int, vp, vp]),
     ("sg_awgn_device", ct.c_int, [ct.c_int, ct.c_uint64, ct.c_uint64, vp, ct.c_int, ct.c_int, ct.c_double, vp, vp]),
     ("sg_bpsk_awgn_llr_device", ct.c_int, [ct.c_int, ct.c_uint64, ct.c_uint64, vp, ct.c_int, ct.c_int, ct.c_double,

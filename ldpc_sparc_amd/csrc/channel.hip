@@ -37,13 +37,14 @@ __global__ __launch_bounds__(256) void rng_bits_kernel(uint64_t seed, uint64_t s
 }
 
 // section index of every logM-bit group, MSB first (bin_arr_2_msg_vector)
-__global__ __launch_bounds__(256) void bits_to_sections_kernel(const uint8_t *bits, int L, int logM, int32_t *idx) {
+__global__ __launch_bounds__(256) void bits_to_sections_kernel(const uint8_t *bits, size_t bit_stride, int L, int logM,
+                                                               int32_t *idx, size_t idx_stride) {
     const int b = blockIdx.y;
     for (int l = blockIdx.x * blockDim.x + threadIdx.x; l < L; l += gridDim.x * blockDim.x) {
-        const uint8_t *x = bits + ((size_t)b * L + l) * logM;
+        const uint8_t *x = bits + (size_t)b * bit_stride + (size_t)l * logM;
         int v = 0;
         for (int j = 0; j < logM; ++j) v = (v << 1) | (x[j] & 1);
-        idx[(size_t)b * L + l] = v;
+        idx[(size_t)b * idx_stride + l] = v;
     }
 }
 
@@ -126,14 +127,21 @@ int sg_rng_bits_device(uint64_t seed, uint64_t stream_id, int B, int nbits, uint
     return SG_OK;
 }
 
-int sg_bits_to_sections_device(const uint8_t *d_bits, int B, int L, int logM, int32_t *d_idx, void *stream) {
+int sg_bits_to_sections_strided_device(const uint8_t *d_bits, size_t bit_stride, int B, int L, int logM,
+                                       int32_t *d_idx, size_t idx_stride, void *stream) {
     SG_CHECK_ARG(d_bits && d_idx && L >= 0 && logM >= 1 && logM <= 30, "bad argument");
+    SG_CHECK_ARG(bit_stride >= (size_t)L * logM && idx_stride >= (size_t)L, "strides shorter than a row");
     if (!B || !L) return SG_OK;
     SG_TRY(ensure_device());
     hipStream_t s = pick_stream(stream);
-    hipLaunchKernelGGL(bits_to_sections_kernel, dim3(grid1(L), B), dim3(256), 0, s, d_bits, L, logM, d_idx);
+    hipLaunchKernelGGL(bits_to_sections_kernel, dim3(grid1(L), B), dim3(256), 0, s, d_bits, bit_stride, L, logM, d_idx,
+                       idx_stride);
     SG_HIP(hipGetLastError());
     return SG_OK;
+}
+
+int sg_bits_to_sections_device(const uint8_t *d_bits, int B, int L, int logM, int32_t *d_idx, void *stream) {
+    return sg_bits_to_sections_strided_device(d_bits, (size_t)L * logM, B, L, logM, d_idx, (size_t)L, stream);
 }
 
 int sg_awgn_device(int precision, uint64_t seed, uint64_t stream_id, const void *d_x, int B, int n, double sigma,

@@ -279,20 +279,28 @@ class ConcatTrial:
     sparc_new.py:15-82) at the points' AWGN variances,
     generated and decoded in batches by pipeline.ConcatPipeline (dense AMP ->
     glue -> batched BP -> device counters).  Block b of point p draws its user
-    bits and noise from default_rng([seed, p, b]), so results do not depend on
-    the rank count.  Counters [codewords, user-bit errors, codeword errors,
+    bits and noise from Philox keyed (seed, p << 32 | b) on the GPU (rng
+    "device", with the LDPC encoder on the GPU too) or from
+    default_rng([seed, p, b]) on the host (rng "host"), so results do not
+    depend on the rank count.  Counters [codewords, user-bit errors, codeword errors,
     unprotected-bit errors, protected-bit errors]; per-block BERs of this
     rank are kept in block_ber[point]."""
 
-    def __init__(self, pipe, awgn_vars, seed=0):
+    def __init__(self, pipe, awgn_vars, seed=0, rng="device"):
         self.pipe, self.vars, self.seed = pipe, list(awgn_vars), int(seed)
         self.user_bits = pipe.L_unp * pipe.logM + pipe.mults * pipe.c.K
         self.block_ber = {}
+        if rng not in ("host", "device"):
+            raise ValueError("rng must be 'host' (numpy default_rng([seed, point, block])) or 'device' (Philox)")
+        self.rng = rng
 
     def __call__(self, point, first_block, n_blocks, block):
         tot = np.zeros(NC, dtype=np.int64)
         for b in range(first_block, first_block + n_blocks):
-            self.pipe.make_batch(block, self.vars[point], np.random.default_rng([self.seed, int(point), int(b)]))
+            if self.rng == "device":  # throughput mode: no host encode or host RNG in the loop
+                self.pipe.make_batch_device(block, self.vars[point], self.seed, (int(point) << 32) | int(b))
+            else:
+                self.pipe.make_batch(block, self.vars[point], np.random.default_rng([self.seed, int(point), int(b)]))
             self.pipe.reset_counts()
             self.pipe.decode()
             c = self.pipe.counts()
@@ -303,7 +311,7 @@ class ConcatTrial:
 
 def concat_ber_sweep(L, M, n, P, L_unprotected, mults, ebn0_db, *, codewords, block=256, blocks_per_round=None,
                      rank=0, world=1, agg=None, design_seed=0, seed=0, t_max=25, bp_its=200, precision="f32",
-                     ldpc=("802.11n", "1/2", 81), min_errors=None, checkpoint_dir=None, npz_file=None):
+                     ldpc=("802.11n", "1/2", 81), min_errors=None, checkpoint_dir=None, npz_file=None, rng="device"):
     """BER / FER of concatenated SPARC + LDPC against Eb/N0 (the experiment of
     ldpc_sparc/performance_plots_general.py:100-138 for the plain concatenated
     decoder), `codewords` per point sharded over the ranks.  Eb/N0 to noise as
@@ -318,7 +326,7 @@ def concat_ber_sweep(L, M, n, P, L_unprotected, mults, ebn0_db, *, codewords, bl
     user_bits = L_unprotected * pipe.logM + mults * pipe.c.K
     r_overall = user_bits / n
     vars_ = [P / (2 * r_overall * 10 ** (e / 10)) for e in ebn0_db]
-    trial = ConcatTrial(pipe, vars_, seed)
+    trial = ConcatTrial(pipe, vars_, seed, rng)
     bpr = blocks_per_round or max(1, world)
     out = []
     for point, e in enumerate(ebn0_db):
@@ -327,7 +335,7 @@ def concat_ber_sweep(L, M, n, P, L_unprotected, mults, ebn0_db, *, codewords, bl
                         tag=f"concat_L{L}_M{M}_n{n}",
                         params={"P": P, "L_unprotected": L_unprotected, "mults": mults, "ebn0_db": float(e),
                                 "seed": seed, "design_seed": design_seed, "t_max": t_max, "bp_its": bp_its,
-                                "precision": precision, "ldpc": list(ldpc), "codewords": codewords})
+                                "precision": precision, "ldpc": list(ldpc), "codewords": codewords, "rng": rng})
         out.append({"ebn0_db": float(e), "awgn_var": vars_[point], "codewords": int(tot[0]),
                     "ber": float(tot[1]) / (tot[0] * user_bits) if tot[0] else None,
                     "fer": float(tot[2]) / tot[0] if tot[0] else None,

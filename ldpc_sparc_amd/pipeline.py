@@ -46,6 +46,8 @@ class ConcatPipeline:
         self.d_app = _native.DeviceBuffer(B * self.mults * c.N * sz)
         self.d_it = _native.DeviceBuffer(B * self.mults * 4)
         self.d_info = _native.DeviceBuffer(B * self.mults * c.K)
+        self.d_unp = _native.DeviceBuffer(max(1, B * self.L_unp * self.logM))
+        self.d_cw = _native.DeviceBuffer(B * self.mults * c.N)
         self.d_cnt = _native.DeviceBuffer(5 * 8)
         self._cap = B
 
@@ -69,6 +71,35 @@ class ConcatPipeline:
         self.d_y.upload(y)
         self.B = B
         return idx, info
+
+    # distinct Philox keys of the parts of a device batch
+    _SEED_INFO = 0x5DEECE66D
+
+    def make_batch_device(self, B, awgn_var, seed, stream_id):
+        """The same batch generated on the GPU (throughput mode, nothing from
+        the host): Philox user bits of the unprotected sections and of the
+        LDPC information words (sparc_new.py:15-51), the systematic LDPC
+        encoder (ldpc.py:400-460) on the device, MSB-first bits -> section
+        indices, x = A beta0, y = x + AWGN.  The draw of codeword b depends only
+        on (seed, stream_id, b): a Monte-Carlo block keyed by (point, block) is
+        the same whatever the rank count."""
+        self._ensure(B)
+        c, logM, lib = self.c, self.logM, _native.lib()
+        off = _native.offset
+        nu = self.L_unp * logM
+        if nu:
+            _native.check(lib.sg_rng_bits_device(seed, stream_id, B, nu, self.d_unp.ptr, None))
+            _native.check(lib.sg_bits_to_sections_strided_device(self.d_unp.ptr, nu, B, self.L_unp, logM,
+                                                                 self.d_true.ptr, self.L, None))
+        _native.check(lib.sg_rng_bits_device(seed ^ self._SEED_INFO, stream_id, B * self.mults, c.K, self.d_info.ptr,
+                                             None))
+        c.encode_device(self.d_info.ptr, B * self.mults, self.d_cw.ptr)
+        _native.check(lib.sg_bits_to_sections_strided_device(self.d_cw.ptr, self.mults * c.N, B, self.L - self.L_unp,
+                                                             logM, off(self.d_true.ptr, 4 * self.L_unp), self.L, None))
+        _native.check(lib.sg_dense_encode_device(self.plan, self.d_true.ptr, B, self.d_x.ptr, None))
+        _native.check(lib.sg_awgn_device(self.prec, seed, stream_id, self.d_x.ptr, B, self.n,
+                                         float(np.sqrt(awgn_var)), self.d_y.ptr, None))
+        self.B = B
 
     def decode(self):
         """One batch: returns nothing; counters accumulate in d_cnt."""

@@ -49,12 +49,16 @@ def test_bp_statistics_match_reference_campaign():
     assert abs(be / (n * c.N) - ber_ref) < 0.35 * ber_ref
 
 
-def test_concat_sweep_rank_invariant():
+@pytest.mark.parametrize("rng", ["device", "host"])
+def test_concat_sweep_rank_invariant(rng):
     """C5 sweep on a small concatenated code (L=80, M=512 -> 1 x LDPC z=27 in 72
     protected sections): the per-point counters do not depend on how the
-    blocks were dealt (two simulated ranks vs one), and BER falls with Eb/N0."""
+    blocks were dealt (two simulated ranks vs one), and BER falls with Eb/N0
+    -- with the batches generated on the GPU (Philox, device LDPC encoder) or
+    on the host (numpy)."""
     from ldpc_sparc_amd import montecarlo
-    kw = dict(codewords=96, block=32, design_seed=3, seed=4, t_max=10, bp_its=50, ldpc=("802.11n", "1/2", 27))
+    kw = dict(codewords=96, block=32, design_seed=3, seed=4, t_max=10, bp_its=50, ldpc=("802.11n", "1/2", 27),
+              rng=rng)
     one = montecarlo.concat_ber_sweep(80, 512, 600, 15.0, 8, 1, [1.0, 6.0], **kw)
     # the same blocks in two shards, summed by hand
     from ldpc_sparc_amd.pipeline import ConcatPipeline
@@ -62,7 +66,7 @@ def test_concat_sweep_rank_invariant():
     ub = 8 * 9 + pipe.c.K
     for p, e in enumerate([1.0, 6.0]):
         var = 15.0 / (2 * (ub / 600) * 10 ** (e / 10))
-        tr = montecarlo.ConcatTrial(pipe, [var] * 2, seed=4)
+        tr = montecarlo.ConcatTrial(pipe, [var] * 2, seed=4, rng=rng)
         a = tr(p, 0, 1, 32) + tr(p, 1, 2, 32)
         assert int(a[0]) == one[p]["codewords"] == 96
         assert abs(float(a[1]) / (96 * ub) - one[p]["ber"]) < 1e-12

@@ -42,3 +42,30 @@ def test_pipeline_equals_per_codeword_decode(precision):
     assert cnt[0] == B
     assert cnt[1] == errs and cnt[2] == cw_err
     assert cnt[3] + cnt[4] == cnt[1]
+
+
+def test_device_batch_encodes_valid_codewords():
+    """make_batch_device (throughput mode): Philox bits, the LDPC encoder on
+    the GPU, MSB-first section indices and AWGN -- the protected sections carry
+    the host QC encoder's codewords of the drawn information words
+    (ldpc.py:400-460), the unprotected sections the drawn bits, the noise has
+    the requested variance, and the draw depends only on (seed, stream)."""
+    L, M, n, Lu = 80, 512, 600, 8
+    pipe = ConcatPipeline(L, M, n, 15.0, Lu, 1, ldpc=("802.11n", "1/2", 27), design_seed=3)
+    c = pipe.c
+    B, var = 64, 0.7
+    pipe.make_batch_device(B, var, 7, (3 << 32) | 5)
+    idx = pipe.d_true.download(np.zeros((B, L), np.int32))
+    info = pipe.d_info.download(np.zeros((B, c.K), np.uint8))
+    unp = pipe.d_unp.download(np.zeros((B, Lu * 9), np.uint8))
+    bits = ((idx[:, :, None] >> np.arange(9)[::-1]) & 1).reshape(B, L * 9)
+    assert np.array_equal(bits[:, :Lu * 9], unp)
+    assert np.array_equal(bits[:, Lu * 9:], c.encode_batch(info.astype(np.int64)))
+    x = pipe.d_x.download(np.zeros((B, n), np.float32)).astype(np.float64)
+    y = pipe.d_y.download(np.zeros((B, n), np.float32)).astype(np.float64)
+    d = y - x
+    assert abs(d.var() - var) < 0.05 * var and abs(d.mean()) < 0.02
+    pipe.make_batch_device(B, var, 7, (3 << 32) | 5)
+    assert np.array_equal(pipe.d_y.download(np.zeros((B, n), np.float32)), y.astype(np.float32))
+    pipe.make_batch_device(B, var, 7, (3 << 32) | 6)
+    assert not np.array_equal(pipe.d_true.download(np.zeros((B, L), np.int32)), idx)
