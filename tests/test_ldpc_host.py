@@ -1,11 +1,15 @@
 """CPU tests: LDPC host logic (protographs, Tanner graph, encoder) and the BP
 oracle against the golden vectors generated from the reference
 (tests/golden/make_golden.py), mirroring ldpc_jossy/py/test_ldpc.py."""
+import os
+
 import numpy as np
 import pytest
 
 from ldpc_sparc_amd.ldpc import code
 from oracle import bp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 ALL_CODES = [("802.16", r, z, p) for z in (3, 27, 54, 81)
              for (r, p) in [("1/2", "A"), ("2/3", "A"), ("2/3", "B"), ("3/4", "A"), ("3/4", "B"),
@@ -132,3 +136,45 @@ def test_lxor_lxfb_oracle(oracle_built):
         L = rng.standard_normal(7) * 3
         assert bp.lxfb(L, 1)[0] == bp.lxfb(L, 1, use_ref=True)[0]
         assert np.array_equal(bp.lxfb(L, 1)[1], bp.lxfb(L, 1, use_ref=True)[1])
+
+
+@pytest.mark.parametrize("std,rate,z", [("802.11n", "1/2", 27), ("802.11n", "5/6", 27), ("802.16", "2/3", 24)])
+def test_oracle_under_sanitizers(tmp_path, std, rate, z):
+    """the CPU restatement (oracle/bp_oracle.c) built with
+    -fsanitize=address,undefined (make -C oracle san) decodes real graphs --
+    every decoder, and Lxfb at the graph's check degree -- without a report,
+    and gives the same results as the normal build."""
+    import subprocess
+    from oracle import bp
+    r = subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle"), "san"], capture_output=True, text=True)
+    if r.returncode != 0:
+        pytest.skip("sanitizer toolchain unavailable: " + r.stderr[-300:])
+    c = code(std, rate, z)
+    rng = np.random.default_rng(3)
+    X = c.encode_batch(rng.integers(0, 2, (4, c.K)))
+    ch = 2 * ((1 - 2 * X) + 0.7 * rng.standard_normal(X.shape)) / 0.49
+    B, max_it, factor = len(ch), 20, 0.7
+    inp, out = tmp_path / "in.bin", tmp_path / "out.bin"
+    with open(inp, "wb") as f:
+        f.write(np.array([c.N, c.Nc, c.Nmsg, B, max_it], np.int32).tobytes())
+        f.write(np.array([factor]).tobytes())
+        for a in (c.vdeg, c.cdeg, c.intrlv):
+            f.write(np.asarray(a, np.int64).tobytes())
+        f.write(np.ascontiguousarray(ch, np.float64).tobytes())
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:verify_asan_link_order=0:abort_on_error=0",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    r = subprocess.run([os.path.join(REPO, "oracle", "_build", "bp_oracle_san"), str(inp), str(out)], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-3000:]
+    raw = open(out, "rb").read()
+    o = 0
+    for kind in ("sumprod", "sumprod2", "minsum", "minsum_refbug"):
+        app = np.frombuffer(raw, np.float64, B * c.N, o).reshape(B, c.N)
+        o += 8 * B * c.N
+        it = np.frombuffer(raw, np.int32, B, o)
+        o += 4 * B
+        if kind == "minsum_refbug":
+            continue  # pinned to the reference library elsewhere (test_minsum_refbug_matches_reference)
+        eapp, eit = bp.decode_batch(kind, ch, c.vdeg, c.cdeg, c.intrlv, max_it, factor)
+        assert np.array_equal(it, eit), kind
+        np.testing.assert_allclose(app, eapp, rtol=1e-12, atol=1e-12, err_msg=kind)
