@@ -107,15 +107,14 @@ __global__ __launch_bounds__(BK_THREADS) void blk_ab(BlkTables tb, AmpBufs<float
     const int c = blockIdx.x, cw = blockIdx.y, tid = threadIdx.x;
     if (!bf.active[cw]) return;
     const float *beta = bf.beta + (size_t)cw * tb.LM + (size_t)c * tb.Mc;
+    // beta_c once for the column's omega transforms (HBM reads it once)
+    float bv[BK_J];
+#pragma unroll
+    for (int i = 0; i < BK_J; ++i) bv[i] = beta[bk_j<EPS>(tid, i)];
     for (int q = tb.col_ptr[c]; q < tb.col_ptr[c + 1]; ++q) {
         const int t = tb.col_t[q];
         const int tl = bk_opaque(tid);
-        // beta_c and the positions of this transform, in flight while the image
-        // clears (beta is re-read from L2 for each transform: holding it in
-        // registers across the FFT would spill)
-        float bv[BK_J];
-#pragma unroll
-        for (int i = 0; i < BK_J; ++i) bv[i] = beta[bk_j<EPS>(tl, i)];
+        // the positions of this transform, in flight while the image clears
         uint32_t pv[BK_J / 2];
         bk_pos_load(tb, t, tl, pv);
         bk_clear(smem, tl);
