@@ -547,7 +547,8 @@ def sc_bench(args, d, comm, cpu_seconds, procs):
                                              "cpu_ser": float((cmap != true[done]).mean()),
                                              "gpu_ser": float((gmap[done] != true[done]).mean()),
                                              "identical_section_decisions": float((cmap == gmap[done]).mean()),
-                                             "t_final_equal": float((ctf == tf[done]).mean())}}
+                                             "t_final_equal": float((ctf == tf[done]).mean()),
+                                             "t_final_max_abs_diff": int(np.abs(ctf - tf[done]).max())}}
     return out
 
 
