@@ -74,6 +74,9 @@ def parse():
     ap.add_argument("--no-r13", action="store_true", help="skip the decodable-rate (R=1.3) C2 companion line")
     ap.add_argument("--sc-batch", type=int, default=256)
     ap.add_argument("--sc-steps", type=int, default=2)
+    ap.add_argument("--no-sc-notebook", action="store_true",
+                    help="skip the notebook geometry (L=2048, w=2^16) spatially coupled line")
+    ap.add_argument("--sc-notebook-batch", type=int, default=64)
     ap.add_argument("--concat-batch", type=int, default=256)
     ap.add_argument("--concat-steps", type=int, default=2)
     ap.add_argument("--concat-ebn0", type=float, default=5.5)
@@ -460,12 +463,12 @@ def bp_variant(args, d, std, rate, z, dectype, prec, ebn0, B, steps, max_it=50, 
 
 # ------------------------------------------------------------------ spatially coupled (C4)
 
-def sc_bench(args, d, comm, cpu_seconds, procs):
+def sc_bench(args, d, comm, cpu_seconds, procs, L=1024, B=None, steps=None, seed_off=7):
     """C4 (BASELINE.json configs[3], sparc_demo_sc_decode_wave): spatially
     coupled SPARC, omega=6, Lambda=32 (W 37x32, 192 transforms of w=2^15),
     L=1024, M=512, R=1.5 (n=6142), P=15, sigma^2=1, t_max=40; block engine
     (amp_block.hip).  Synthetic inputs generated on the GPU as for C2."""
-    L, M, P, omega, Lam, logM = 1024, 512, 15.0, 6, 32, 9
+    M, P, omega, Lam, logM = 512, 15.0, 6, 32, 9
     W = sparc.sc_basic(np.array(P), omega, Lam)
     Lr, Lc = W.shape
     n = int(round(L * logM / args.rate))
@@ -475,15 +478,18 @@ def sc_bench(args, d, comm, cpu_seconds, procs):
     op = sparc.DesignOperator(W, L, M, n, o0, o1)
     plan = op.plan(_native.SG_F32)
     lib = _native.lib()
-    B, t_max = args.sc_batch, 40
+    B, t_max = (B or args.sc_batch), 40
+    steps = steps or args.sc_steps
+    engine = {0: "general four-step (amp_dct.hip)", 3: "block (amp_block.hip)"}.get(
+        lib.sg_amp_plan_engine(plan, B), "?")
     d_bits = _native.DeviceBuffer(B * L * logM)
     d_true = _native.DeviceBuffer(B * L * 4)
     d_x = _native.DeviceBuffer(B * n * 4)
     d_y = _native.DeviceBuffer(B * n * 4)
-    _native.check(lib.sg_rng_bits_device(args.seed + 7, d.rank, B, L * logM, d_bits.ptr, None))
+    _native.check(lib.sg_rng_bits_device(args.seed + seed_off, d.rank, B, L * logM, d_bits.ptr, None))
     _native.check(lib.sg_bits_to_sections_device(d_bits.ptr, B, L, logM, d_true.ptr, None))
     _native.check(lib.sg_amp_encode_device(plan, d_true.ptr, B, d_x.ptr, None))
-    _native.check(lib.sg_awgn_device(_native.SG_F32, args.seed + 7, d.rank, d_x.ptr, B, n, 1.0, d_y.ptr, None))
+    _native.check(lib.sg_awgn_device(_native.SG_F32, args.seed + seed_off, d.rank, d_x.ptr, B, n, 1.0, d_y.ptr, None))
     d_map, d_tf, d_cnt = _native.DeviceBuffer(B * L * 4), _native.DeviceBuffer(B * 4), _native.DeviceBuffer(32)
 
     def step():
@@ -501,22 +507,23 @@ def sc_bench(args, d, comm, cpu_seconds, procs):
     d.barrier()
     _native.device_synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.sc_steps):
+    for _ in range(steps):
         step()
     _native.device_synchronize()
     el = d.max(time.perf_counter() - t0)
     ph = prof.stop()
     tf = d_tf.download(np.zeros(B, np.int32))
     cnt = d_cnt.download(np.zeros(4, np.int64))
-    cw_it = int(tf.sum()) * args.sc_steps
+    cw_it = int(tf.sum()) * steps
     kms = sum(ph.get(k, (0.0, 0))[0] for k in AMP_PHASES)
     w = int(op.w)
     sc_traffic, sc_tfile = pmc_traffic("sc", "hbm_bytes_per_codeword_iteration_approx")
     flops = 2 * int(np.count_nonzero(W)) * 2.5 * w * np.log2(w) + 20 * L * M  # per codeword-iteration
     ach = flops * cw_it / (kms * 1e-3) / 1e12 if kms else None
-    out = {"workload": "C4: spatially coupled SPARC (omega=6, Lambda=32, W 37x32, 192 transforms of w=2^15), "
-                       f"L=1024, M=512, R={args.rate} (n={n}), P=15, sigma^2=1, t_max=40",
-           "value": d.world * B * args.sc_steps / el, "unit": "codewords/s", "batch_per_gpu": B,
+    out = {"workload": f"spatially coupled SPARC (omega=6, Lambda=32, W 37x32, 192 transforms of w=2^{int(np.log2(w))}), "
+                       f"L={L}, M=512, R={args.rate} (n={n}), P=15, sigma^2=1, t_max=40",
+           "engine": engine,
+           "value": d.world * B * steps / el, "unit": "codewords/s", "batch_per_gpu": B,
            "avg_iterations": float(tf.mean()), "section_errors": int(cnt[0]), "codeword_errors": int(cnt[2]),
            "ser": float(cnt[0]) / (d.world * B * L),
            "roofline": {"bound": "valu-f32", "achieved": ach, "peak": VALU_PEAK_TFS, "unit": "TFLOP/s",
@@ -524,7 +531,8 @@ def sc_bench(args, d, comm, cpu_seconds, procs):
                         "traffic": sc_traffic,
                         "traffic_unit": "HBM bytes per codeword-iteration, block-engine kernels (PMC, "
                                         f"profiles/{sc_tfile})",
-                        "kernel": "blk_ab + blk_g + blk_az + control (amp_block.hip)",
+                        "kernel": "blk_ab + blk_g + blk_az + control (amp_block.hip)" if "block" in engine else
+                                  "general four-step kernels (amp_dct.hip)",
                         "algorithmic_flops_per_codeword_iteration": flops,
                         "note": "2 nT transforms x 2.5 w log2 w + 20 L M per codeword-iteration; each transform "
                                 "runs in one workgroup's LDS, so HBM sees only beta, z and the tables",
@@ -540,7 +548,7 @@ def sc_bench(args, d, comm, cpu_seconds, procs):
         cmap = np.stack([res[b][0] for b in done])
         ctf = np.array([res[b][1] for b in done])
         out["cpu_baseline"] = {"value": len(done) / cel, "unit": "codewords/s", "cores": procs, "kind": "port",
-                               "sample": f"{len(done)} C4 codewords ({int(ctf.sum())} AMP iterations, {cel:.1f} s "
+                               "sample": f"{len(done)} codewords of this geometry ({int(ctf.sum())} AMP iterations, {cel:.1f} s "
                                          "wall) decoded by oracle/sparc_ref.py (scipy fftpack DCT per block, float128 "
                                          f"softmax), one single-threaded process per core on {procs} host cores",
                                "ber_match": {"codewords": len(done),
@@ -796,6 +804,9 @@ def main():
 
     if not args.no_sc:
         out["sc"] = sc_bench(args, d, comm, 0.4 * args.cpu_seconds if cpu_on else 0, procs)
+    if not args.no_sc_notebook:  # sparc_demo_sc_decode_wave.ipynb cell 1: the reference's published M=512 setup
+        out["sc_notebook"] = sc_bench(args, d, comm, 0.2 * args.cpu_seconds if cpu_on else 0, procs, L=2048,
+                                      B=args.sc_notebook_batch, steps=1, seed_off=9)
 
     if not args.no_concat:
         out["concat"] = concat_bench(args, d)

@@ -206,10 +206,10 @@ def test_full_size_decode_f64_vs_oracle():
     assert np.mean(mi[0] != np.argmax(rb.reshape(L, M), 1)) < 0.01
 
 
-def _c4_design(seed, R=1.5):
+def _c4_design(seed, R=1.5, L=1024):
     """C4 geometry (sparc_demo_sc_decode_wave): spatially coupled omega=6,
     Lambda=32, L=1024, M=512 -> W 37x32, Mr=166, n=6142, Mc=16384, w=2^15."""
-    L, M, P, omega, Lam = 1024, 512, 15.0, 6, 32
+    M, P, omega, Lam = 512, 15.0, 6, 32
     W = sparc.sc_basic(np.array(P), omega, Lam)
     Lr, Lc = W.shape
     n = int(round(L * 9 / R))
@@ -262,6 +262,46 @@ def test_c4_block_engine_vs_general_engine(monkeypatch):
     assert np.mean(mb != mg) < 1e-3
     np.testing.assert_allclose(nb[:, :10], ng[:, :10], atol=1e-4)
     assert np.mean(mb != true) < 0.05  # the decode wave runs through at R = 1.5
+
+
+def _notebook_design(seed):
+    """The notebook's own geometry (sparc_demo_sc_decode_wave.ipynb cell 1):
+    spatially coupled omega=6, Lambda=32, L=2048, M=512, R=1.5, P=15 ->
+    W 37x32, Mr=332, n=12284, Mc=32768, w=2^16 (the general four-step path)."""
+    return _c4_design(seed, L=2048)
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_notebook_geometry_vs_oracle(precision):
+    """The reference's only published M=512 configuration, one codeword of the
+    notebook's geometry against the CPU restatement of sparc.py:883-999:
+    f64 -- same t_final and MAP decisions, NMSE within 1e-9; f32 -- t_final
+    within 2, decisions on all but 0.5 % of the sections, NMSE within 2e-3
+    over the first 10 iterations."""
+    W, L, M, n, o0, o1 = _notebook_design(13)
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    assert op.w == 2 ** 16 and W.shape == (37, 32) and n == 12284
+    prec = _native.SG_F64 if precision == "f64" else _native.SG_F32
+    assert _native.lib().sg_amp_plan_engine(op.plan(prec), 1) == 0  # the general path
+    Ab, Az = sparc_ref.dct_operators(W, L, M, n, o0, o1)
+    rng = np.random.RandomState(14)
+    true = rng.randint(0, M, L)
+    beta0 = np.zeros(L * M)
+    beta0[np.arange(L) * M + true] = 1
+    y = Ab(beta0) + rng.randn(n)
+    rb, rt, rn, rp = sparc_ref.amp(y, W, L, M, n, 1.0, 40, Ab, Az, beta0)
+    mi, tf, nm, ps = sparc.amp_decode_batch(y[None], op, 1.0, 40, true_idx=true[None], precision=prec)
+    ref_map = np.argmax(rb.reshape(L, M), 1)
+    rn = np.asarray(rn).reshape(40, -1)
+    if precision == "f64":
+        assert int(tf[0]) == int(rt)
+        assert np.array_equal(mi[0], ref_map)
+        np.testing.assert_allclose(nm[0], rn, atol=1e-9)
+    else:
+        assert abs(int(tf[0]) - int(rt)) <= 2, (tf[0], rt)
+        assert np.mean(mi[0] != ref_map) < 0.005
+        np.testing.assert_allclose(nm[0, :10], rn[:10], atol=2e-3)
+    assert np.mean(ref_map != true) < 0.01  # the decode wave runs through at this size
 
 
 # ---- per-codeword engine (amp_cw.hip): opt-in with SG_AMP_ENGINE=cw (plan
