@@ -76,7 +76,7 @@ def parse():
     ap.add_argument("--sc-steps", type=int, default=2)
     ap.add_argument("--no-sc-notebook", action="store_true",
                     help="skip the notebook geometry (L=2048, w=2^16) spatially coupled line")
-    ap.add_argument("--sc-notebook-batch", type=int, default=64)
+    ap.add_argument("--sc-notebook-batch", type=int, default=256)
     ap.add_argument("--concat-batch", type=int, default=256)
     ap.add_argument("--concat-steps", type=int, default=2)
     ap.add_argument("--concat-ebn0", type=float, default=5.5)
@@ -480,7 +480,8 @@ def sc_bench(args, d, comm, cpu_seconds, procs, L=1024, B=None, steps=None, seed
     lib = _native.lib()
     B, t_max = (B or args.sc_batch), 40
     steps = steps or args.sc_steps
-    engine = {0: "general four-step (amp_dct.hip)", 3: "block (amp_block.hip)"}.get(
+    engine = {0: "general four-step (amp_dct.hip)",
+              3: "block (amp_block.hip)" if int(op.w) <= 2 ** 15 else "two-class block (amp_block2.hip)"}.get(
         lib.sg_amp_plan_engine(plan, B), "?")
     d_bits = _native.DeviceBuffer(B * L * logM)
     d_true = _native.DeviceBuffer(B * L * 4)
@@ -531,7 +532,8 @@ def sc_bench(args, d, comm, cpu_seconds, procs, L=1024, B=None, steps=None, seed
                         "traffic": sc_traffic,
                         "traffic_unit": "HBM bytes per codeword-iteration, block-engine kernels (PMC, "
                                         f"profiles/{sc_tfile})",
-                        "kernel": "blk_ab + blk_g + blk_az + control (amp_block.hip)" if "block" in engine else
+                        "kernel": ("blk2_ab + blk_g + blk2_az + control (amp_block2.hip)" if "two-class" in engine else
+                                   "blk_ab + blk_g + blk_az + control (amp_block.hip)") if "block" in engine else
                                   "general four-step kernels (amp_dct.hip)",
                         "algorithmic_flops_per_codeword_iteration": flops,
                         "note": "2 nT transforms x 2.5 w log2 w + 20 L M per codeword-iteration; each transform "

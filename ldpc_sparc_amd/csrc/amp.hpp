@@ -45,12 +45,14 @@ struct BlkTables {
     const int32_t *gptr;      // [nT + 1] G slots of each transform (CSR)
     const int32_t *grow;      // row block of each slot's transform
     const uint16_t *gloc;     // fsw(k) of the slot
+    const int32_t *gk;        // k of the slot (two-class form, amp_block2.hip)
     const int32_t *gi;        // [4] per slot: contributing output row index (local to the row block) or -1
     const cx<float> *gc;      // [4] per slot: coefficient
     const cx<float> *stw;     // per-stage twiddles of the N2-point FFT (fft.hpp lds_fft1_ct, EPT 16)
     int skip;                 // timing ablation only (SG_AMP_SKIP): 1 sections, 2 inverse FFT
 };
 size_t blk_lds_bytes(int Mc);
+size_t blk2_lds_bytes();
 
 // Per-batch device buffers.
 template <typename T>
@@ -221,7 +223,11 @@ template <typename T>
 int amp_launch_uncast(const T *in, double *out, size_t n, hipStream_t s);
 int blk_launch_ab(const BlkTables &tb, const AmpBufs<float> &bf, hipStream_t s);   // beta -> rbuf
 int blk_launch_az(const BlkTables &tb, const AmpBufs<float> &bf, cx<float> *gbuf,
-                  hipStream_t s);  // z/phi -> G slots (gbuf [B][ngs]) -> beta, section statistics
+                  hipStream_t s);
+int blk_launch_g(const BlkTables &tb, const AmpBufs<float> &bf, cx<float> *gbuf, hipStream_t s);  // G slots
+// two-class form for w = 2^16 (amp_block2.hip)
+int blk2_launch_ab(const BlkTables &tb, const AmpBufs<float> &bf, hipStream_t s);
+int blk2_launch_az(const BlkTables &tb, const AmpBufs<float> &bf, cx<float> *gbuf, hipStream_t s);  // z/phi -> G slots (gbuf [B][ngs]) -> beta, section statistics
 int amp_launch_count(const int32_t *map_idx, const int32_t *true_idx, const int32_t *t_final, int B, int L,
                      int logM, int64_t *counts, hipStream_t s);
 

@@ -332,14 +332,18 @@ int blk_launch_ab(const BlkTables &tb, const AmpBufs<float> &bf, hipStream_t s) 
     return SG_OK;
 }
 
+int blk_launch_g(const BlkTables &tb, const AmpBufs<float> &bf, cx<float> *gbuf, hipStream_t s) {
+    if (bf.B <= 0) return SG_OK;
+    ProfScope ps(SG_PH_AZ_A, s);
+    hipLaunchKernelGGL(blk_g, dim3((tb.ngs + 255) / 256, bf.B), dim3(256), 0, s, tb, bf, gbuf);
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
 int blk_launch_az(const BlkTables &tb, const AmpBufs<float> &bf, cx<float> *gbuf, hipStream_t s) {
     if (bf.B <= 0) return SG_OK;
     const size_t lds = blk_lds_bytes(tb.Mc);
-    {
-        ProfScope ps(SG_PH_AZ_A, s);
-        hipLaunchKernelGGL(blk_g, dim3((tb.ngs + 255) / 256, bf.B), dim3(256), 0, s, tb, bf, gbuf);
-    }
-    SG_HIP(hipGetLastError());
+    SG_TRY(blk_launch_g(tb, bf, gbuf, s));
     int rc = SG_OK;
     ProfScope ps(SG_PH_AZ_B, s);
     BK_EPS_DISPATCH(tb.M, bk_launch_az, tb, bf, (const cx<float> *)gbuf, lds, s, &rc);

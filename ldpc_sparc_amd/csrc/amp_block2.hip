@@ -1,0 +1,313 @@
+// Block engine, two-class form: AMP for spatially coupled sub-sampled DCT
+// designs whose transforms have w = 2^16 (N2 = 2^15 complex points) -- the
+// geometry of the reference's notebook (sparc_demo_sc_decode_wave.ipynb
+// cell 1: omega = 6, Lambda = 32, L = 2048, M = 512; sparc.py:535-568
+// sc_basic, :851-875 the per-block operators).  A 2^15-point image does not
+// fit one workgroup's LDS, so every transform runs as two classes of 2^14
+// points (the per-codeword engine's class decomposition, amp_cw.hip):
+//   packed input v[m], m = 2 m1 + m2:  H[k] = sum_m2 w_N2^(m2 k) Y_m2[k mod P],
+//   Y_m2 = the P-point FFT of class m2 (P = 2^14, in LDS);
+//   inverse: x[2 m1 + m2] = P-point inverse FFT over k1 of
+//            U_m2[k1] = sum_{k = k1 mod P} G[k] conj(w_N2^(m2 k)).
+// Reference: sparc_public/sparc.py sparc_amp :883-999, sub_dct :648-701,
+// msg_vector_mmse_estimator :402-465, msg_vector_map_estimator :467-512.
+//
+// One 1024-thread workgroup owns one column block c (Mc = 32768 entries, 32
+// a thread) of one codeword and runs its omega transforms, each class in turn:
+//   blk2_ab  for each transform and class: beta of the class's column entries
+//            -> scatter -> three radix-16 stages -> the Mr needed outputs with
+//            the last radix-4 stage and the class factor folded into their
+//            coefficients, summed over the classes in registers -> rbuf[t]
+//   blk2_az  for each transform and class: the class's rows of G (at most two
+//            slots per row, k1 and k1 + P) -> inverse FFT -> the class's column
+//            entries gathered into u (registers); then the column's sections:
+//            s = beta + tau_c u, softmax, MAP, section statistics (amp_block.hip)
+#include "amp.hpp"
+
+namespace sg {
+
+constexpr int B2_THREADS = 1024;
+constexpr int B2_LOG2P = 14, B2_P = 1 << B2_LOG2P;
+constexpr int B2_J = 32;  // column entries per thread (Mc = 32768)
+
+namespace {
+
+template <typename T>
+__device__ __forceinline__ T b2_wave_max(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ T b2_wave_sum(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ int b2_wave_min(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__device__ __forceinline__ int b2_opaque(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+__device__ __forceinline__ void b2_clear(unsigned char *smem, int tid) {
+#pragma unroll
+    for (int i = 0; i < B2_P * (int)sizeof(cx<float>) / 16 / B2_THREADS; ++i)
+        reinterpret_cast<uint4 *>(smem)[tid + i * B2_THREADS] = uint4{0, 0, 0, 0};
+}
+
+// Column entry i (< 32) of thread tid: wavefront w owns sections
+// w spw .. w spw + spw - 1 of the column block (spw = 2048 / M), lane l holds
+// entries l eps .. l eps + eps - 1 of each (eps = M / 64).  Host mirror in
+// capi_amp.cpp build_block2.
+template <int EPS>
+__device__ __forceinline__ int b2_j(int tid, int i) {
+    constexpr int M = 64 * EPS, SPW = 2048 / M;
+    const int sq = i / EPS, e = i - sq * EPS;
+    return ((tid >> 6) * SPW + sq) * M + (tid & 63) * EPS + e;
+}
+
+// class bit (15) | real LDS index in the class image (2 fsw(m1) + component)
+// of the thread's column entries of transform t, packed in pairs
+__device__ __forceinline__ void b2_pos_load(const BlkTables &tb, int t, int tid, uint32_t *pv) {
+    const uint32_t *p2 = tb.pos2 + (size_t)t * (B2_J / 2) * B2_THREADS;
+#pragma unroll
+    for (int i = 0; i < B2_J / 2; ++i) pv[i] = p2[i * B2_THREADS + tid];
+}
+__device__ __forceinline__ uint32_t b2_pos(const uint32_t *pv, int i) { return (pv[i >> 1] >> (16 * (i & 1))) & 0xffffu; }
+
+// the first three stages (radix 16) of the P-point FFT, as amp_block.hip
+__device__ __forceinline__ void b2_fwd_stages(cx<float> *d, const cx<float> *__restrict__ stw, int tid) {
+    cx<float> w0[1], w1[6], w2[6];
+    fft1_tw_load_ct<float, 16, B2_LOG2P, 1>(stw, tid, w1);
+    stockham1_stage_ct<float, false, 16, 16, B2_LOG2P, 0>(d, w0, tid);
+    fft1_tw_load_ct<float, 16, B2_LOG2P, 2>(stw, tid, w2);
+    stockham1_stage_ct<float, false, 16, 16, B2_LOG2P, 4>(d, w1, tid);
+    stockham1_stage_ct<float, false, 16, 16, B2_LOG2P, 8>(d, w2, tid);
+}
+
+}  // namespace
+
+size_t blk2_lds_bytes() { return (size_t)B2_P * sizeof(cx<float>); }
+
+// ------------------------------------------------------------------ Ab
+template <int EPS>
+__global__ __launch_bounds__(B2_THREADS) void blk2_ab(BlkTables tb, AmpBufs<float> bf) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cx<float> *d = reinterpret_cast<cx<float> *>(smem);
+    float *dr = reinterpret_cast<float *>(smem);
+    const int c = blockIdx.x, cw = blockIdx.y, tid = threadIdx.x;
+    if (!bf.active[cw]) return;
+    const float *beta = bf.beta + (size_t)cw * tb.LM + (size_t)c * tb.Mc;
+    for (int q = tb.col_ptr[c]; q < tb.col_ptr[c + 1]; ++q) {
+        const int t = tb.col_t[q];
+        float acc = 0.f;  // output tid (Mr <= 1024), summed over the two classes
+        for (int m2 = 0; m2 < 2; ++m2) {
+            const int tl = b2_opaque(tid);
+            // beta_c and the positions, in flight while the image clears
+            float bv[B2_J];
+#pragma unroll
+            for (int i = 0; i < B2_J; ++i) bv[i] = beta[b2_j<EPS>(tl, i)];
+            uint32_t pv[B2_J / 2];
+            b2_pos_load(tb, t, tl, pv);
+            b2_clear(smem, tl);
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < B2_J; ++i) {
+                const uint32_t p = b2_pos(pv, i);
+                if ((int)(p >> 15) == m2) dr[p & 0x7fffu] = bv[i];
+            }
+            __syncthreads();
+            b2_fwd_stages(d, tb.stw, tl);
+            // X_i += Re(sum_r al_r Y[a mod 4096 + 4096 r] + be_r conj Y[b mod ...]):
+            // the radix-4 stage and w_N2^(m2 k) are in the coefficients
+            if (tl < tb.Mr) {
+                const uint32_t ab = tb.oab[(size_t)t * tb.Mr + tl];
+                const int ja = ab & 0xffffu, jb = ab >> 16;
+                const cx<float> *oc = tb.oc + (((size_t)t * 2 + m2) * tb.Mr + tl) * 8;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const cx<float> ya = d[fsw(ja + 4096 * r)], yb = d[fsw(jb + 4096 * r)];
+                    const cx<float> al = oc[r], be = oc[4 + r];
+                    acc += (al.x * ya.x - al.y * ya.y) + (be.x * yb.x + be.y * yb.y);
+                }
+            }
+            __syncthreads();
+        }
+        if (tid < tb.Mr) bf.rbuf[((size_t)cw * tb.nT + t) * tb.Mr + tid] = acc;
+    }
+}
+
+// ------------------------------------------------------------------ Az + eta
+template <int EPS>
+__global__ __launch_bounds__(B2_THREADS) void blk2_az(BlkTables tb, AmpBufs<float> bf, const cx<float> *gbuf) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cx<float> *d = reinterpret_cast<cx<float> *>(smem);
+    float *dr = reinterpret_cast<float *>(smem);
+    const int c = blockIdx.x, cw = blockIdx.y, tid = threadIdx.x;
+    if (!bf.active[cw]) return;
+    float u[B2_J];
+#pragma unroll
+    for (int i = 0; i < B2_J; ++i) u[i] = 0.f;
+    const cx<float> *gcw = gbuf + (size_t)cw * tb.ngs;
+    const float inv_n2 = 1.0f / (float)(2 * B2_P);
+    for (int q = tb.col_ptr[c]; q < tb.col_ptr[c + 1]; ++q) {
+        const int t = tb.col_t[q];
+        const int g0 = tb.gptr[t], ng = tb.gptr[t + 1] - g0;
+        for (int m2 = 0; m2 < 2; ++m2) {
+            const int tl = b2_opaque(tid);
+            b2_clear(smem, tl);
+            __syncthreads();
+            // rows of class m2: U[k1] = sum over k = k1 mod P of G[k] conj(w_N2^(m2 k));
+            // at most two slots (k1, k1 + P) share a row, and two float additions
+            // onto a zero commute, so the atomic sum is deterministic
+            for (int g = tl; g < ng; g += B2_THREADS) {
+                const int k = tb.gk[g0 + g];
+                cx<float> v = gcw[g0 + g];
+                if (m2) {
+                    const float x = (float)k * inv_n2;  // conj(w_N2^k) = exp(+2 pi i k / N2)
+                    const float cs = __builtin_amdgcn_cosf(x), sn = __builtin_amdgcn_sinf(x);
+                    v = {v.x * cs - v.y * sn, v.x * sn + v.y * cs};
+                }
+                cx<float> *dst = &d[fsw(k & (B2_P - 1))];
+                atomicAdd(&dst->x, v.x);
+                atomicAdd(&dst->y, v.y);
+            }
+            __syncthreads();
+            lds_fft1_ct_lean<float, true, 16, B2_LOG2P>(d, tb.stw, tl);  // no twiddles in flight: u[] stays in registers
+            uint32_t pv[B2_J / 2];
+            b2_pos_load(tb, t, tl, pv);
+#pragma unroll
+            for (int i = 0; i < B2_J; ++i) {
+                const uint32_t p = b2_pos(pv, i);
+                if ((int)(p >> 15) == m2) u[i] += dr[p & 0x7fffu];
+            }
+            __syncthreads();
+        }
+    }
+    // ---- sections of the column block (sparc.py:972, :429-432, :485-487), one
+    // at a time: s = beta + tau u, x = s / tau, beta = exp(x - max) / sum, MAP =
+    // first index of max s.  A wavefront owns whole sections (b2_j).
+    const int lane = tid & 63, wv = tid >> 6;
+    constexpr int eps = EPS, spw = 2048 / (64 * EPS);
+    const int nsec = tb.Mc / tb.M;
+    const float tau = (float)bf.tau[(size_t)cw * tb.Lc + c];
+    float *beta = bf.beta + (size_t)cw * tb.LM + (size_t)c * tb.Mc;
+    const int l0 = c * nsec;  // first section of the column block
+#pragma unroll
+    for (int sq = 0; sq < spw; ++sq) {
+        const int ls = wv * spw + sq;  // section within the column block
+        const int i0 = sq * eps;
+        float s[eps], x[eps];
+#pragma unroll
+        for (int e = 0; e < eps; ++e) {
+            s[e] = beta[ls * tb.M + lane * eps + e] + tau * u[i0 + e];  // sparc.py:972
+            x[e] = s[e] / tau;                                          // sparc.py:430
+        }
+        float xm = -INFINITY, sm = -INFINITY;
+        int arg = 0x7fffffff;
+#pragma unroll
+        for (int e = 0; e < eps; ++e) {
+            xm = fmax(xm, x[e]);
+            if (s[e] > sm) {
+                sm = s[e];
+                arg = lane * eps + e;
+            }
+        }
+        xm = b2_wave_max(xm);
+        const float gm = b2_wave_max(sm);
+        arg = b2_wave_min(sm == gm ? arg : 0x7fffffff);
+        float dn = 0.f;
+#pragma unroll
+        for (int e = 0; e < eps; ++e) {
+            x[e] = __expf(x[e] - xm);
+            dn += x[e];
+        }
+        dn = b2_wave_sum(dn);
+        const int truth = bf.true_idx ? bf.true_idx[(size_t)cw * tb.L + l0 + ls] : -1;
+        float ss = 0.f, se = 0.f;
+#pragma unroll
+        for (int e = 0; e < eps; ++e) {
+            const float b = x[e] / dn;
+            beta[ls * tb.M + lane * eps + e] = b;
+            const float dl = b - ((lane * eps + e) == truth ? 1.f : 0.f);
+            ss += b * b;
+            se += dl * dl;
+        }
+        ss = b2_wave_sum(ss);
+        se = b2_wave_sum(se);
+        if (lane == 0) {
+            const size_t o = (size_t)cw * tb.L + l0 + ls;
+            bf.sec_sumsq[o] = (double)ss;
+            bf.sec_err[o] = (double)se;
+            bf.sec_argmax[o] = arg;
+        }
+    }
+}
+
+template <int EPS>
+static int blk2_set_attrs(size_t lds) {
+    static size_t done = 0;
+    if (done >= lds) return SG_OK;
+    SG_HIP(hipFuncSetAttribute((const void *)blk2_ab<EPS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    SG_HIP(hipFuncSetAttribute((const void *)blk2_az<EPS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    done = lds;
+    return SG_OK;
+}
+
+// section size M = 64 EPS, 64 <= M <= 2048
+#define B2_EPS_DISPATCH(M, F, ...)                                                              \
+    switch (M) {                                                                                \
+    case 64: F<1>(__VA_ARGS__); break;                                                          \
+    case 128: F<2>(__VA_ARGS__); break;                                                         \
+    case 256: F<4>(__VA_ARGS__); break;                                                         \
+    case 512: F<8>(__VA_ARGS__); break;                                                         \
+    case 1024: F<16>(__VA_ARGS__); break;                                                       \
+    case 2048: F<32>(__VA_ARGS__); break;                                                       \
+    default: return fail(SG_ERR_UNSUPPORTED, "block engine (two classes): section size M=%d", M); \
+    }
+
+template <int EPS>
+static void b2_launch_ab(const BlkTables &tb, const AmpBufs<float> &bf, size_t lds, hipStream_t s, int *rc) {
+    *rc = blk2_set_attrs<EPS>(lds);
+    if (*rc == SG_OK) hipLaunchKernelGGL(blk2_ab<EPS>, dim3(tb.Lc, bf.B), dim3(B2_THREADS), lds, s, tb, bf);
+}
+template <int EPS>
+static void b2_launch_az(const BlkTables &tb, const AmpBufs<float> &bf, const cx<float> *gbuf, size_t lds,
+                         hipStream_t s, int *rc) {
+    *rc = blk2_set_attrs<EPS>(lds);
+    if (*rc == SG_OK) hipLaunchKernelGGL(blk2_az<EPS>, dim3(tb.Lc, bf.B), dim3(B2_THREADS), lds, s, tb, bf, gbuf);
+}
+
+int blk2_launch_ab(const BlkTables &tb, const AmpBufs<float> &bf, hipStream_t s) {
+    if (bf.B <= 0) return SG_OK;
+    if (tb.Mc != 2 * B2_P || tb.Mr > B2_THREADS)
+        return fail(SG_ERR_UNSUPPORTED, "block engine (two classes): Mc=%d, Mr=%d", tb.Mc, tb.Mr);
+    const size_t lds = blk2_lds_bytes();
+    int rc = SG_OK;
+    ProfScope ps(SG_PH_AB_A, s);
+    B2_EPS_DISPATCH(tb.M, b2_launch_ab, tb, bf, lds, s, &rc);
+    SG_TRY(rc);
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
+int blk2_launch_az(const BlkTables &tb, const AmpBufs<float> &bf, cx<float> *gbuf, hipStream_t s) {
+    if (bf.B <= 0) return SG_OK;
+    if (tb.Mc != 2 * B2_P) return fail(SG_ERR_UNSUPPORTED, "block engine (two classes): Mc=%d", tb.Mc);
+    SG_TRY(blk_launch_g(tb, bf, gbuf, s));
+    const size_t lds = blk2_lds_bytes();
+    int rc = SG_OK;
+    ProfScope ps(SG_PH_AZ_B, s);
+    B2_EPS_DISPATCH(tb.M, b2_launch_az, tb, bf, (const cx<float> *)gbuf, lds, s, &rc);
+    SG_TRY(rc);
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
+}  // namespace sg

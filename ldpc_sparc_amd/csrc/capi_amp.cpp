@@ -71,6 +71,8 @@ struct sg_amp_plan {
     void *c_gc = nullptr, *c_stw = nullptr;
     // block engine (several transforms per column block, amp_block.hip)
     bool block = false;
+    bool block2 = false;         // two-class block engine (w = 2^16, amp_block2.hip)
+    int32_t *b_gk = nullptr;
     uint16_t *b_gloc = nullptr;
     uint32_t *b_pos2 = nullptr, *b_oab = nullptr;
     int32_t *b_gptr = nullptr, *b_gi = nullptr, *b_grow = nullptr;
@@ -212,7 +214,7 @@ static int ensure_ws(sg_amp_plan *p, int B, int t_max) {
         SG_ALLOC(p->ws_sumsq, Bz * p->L * 8);
         SG_ALLOC(p->ws_err, Bz * p->L * 8);
     }
-    if (p->block) SG_ALLOC(p->ws_gbuf, Bz * (size_t)p->b_ngs * 8);
+    if (p->block || p->block2) SG_ALLOC(p->ws_gbuf, Bz * (size_t)p->b_ngs * 8);
     SG_ALLOC(p->ws_phi, Bz * p->Lr * 8);
     SG_ALLOC(p->ws_tau, Bz * p->Lc * 8);
     SG_ALLOC(p->ws_psi, Bz * p->Lc * 8);
@@ -265,6 +267,7 @@ static BlkTables btables(const sg_amp_plan *p) {
     tb.col_ptr = p->col_ptr; tb.col_t = p->col_t; tb.t_row = p->t_row;
     tb.pos2 = p->b_pos2; tb.oab = p->b_oab; tb.oc = (const cx<float> *)p->b_oc;
     tb.ngs = p->b_ngs; tb.gptr = p->b_gptr; tb.grow = p->b_grow; tb.gloc = p->b_gloc; tb.gi = p->b_gi; tb.gc = (const cx<float> *)p->b_gc;
+    tb.gk = p->b_gk;
     tb.stw = (const cx<float> *)p->b_stw;
     tb.skip = diag_skip();
     return tb;
@@ -755,6 +758,87 @@ static int build_block(sg_amp_plan *p, const uint32_t *order0, const uint32_t *o
     return SG_OK;
 }
 
+// Tables of the two-class block engine (amp_block2.hip): w = 2^16, N2 = 2 P with
+// P = 2^14.  Column entry j sits at packed slot m = 2 m1 + m2 of its transform:
+// class m2, real LDS index 2 fsw(m1) + component in the class image; owned by
+// (thread, entry) as b2_j.  Output coefficients per class fold the class
+// factor w_N2^(m2 k) and the last radix-4 stage: al = c1 w_N2^((m2 + 2 r) a).
+static int build_block2(sg_amp_plan *p, const uint32_t *order0, const uint32_t *order1,
+                        const std::vector<double> &t_scale, const std::vector<int32_t> &row_of) {
+    const long long N = p->w, N2 = p->N2;
+    const int nT = p->nT, Mc = p->Mc, Mr = p->Mr, M = p->M;
+    constexpr int J = 32, T = 1024;
+    std::vector<uint32_t> pos2((size_t)nT * (J / 2) * T, 0u);
+    std::vector<uint32_t> oab((size_t)nT * Mr);
+    std::vector<cd> oc((size_t)nT * 2 * Mr * 8), gc;
+    std::vector<int32_t> gptr(nT + 1, 0), gi, grow, gk;
+    std::vector<uint16_t> gloc;
+    const int eps = M / 64, spw = 2048 / M;
+    for (int t = 0; t < nT; ++t) {
+        const uint32_t *o0 = order0 + (size_t)t * Mr, *o1 = order1 + (size_t)t * Mc;
+        for (int j = 0; j < Mc; ++j) {
+            const long long sl = slot_of_pos(o1[j], N);
+            const long long m = sl >> 1;
+            const uint32_t lds = (uint32_t)(2 * fsw((int)(m >> 1)) + (int)(sl & 1)) | ((uint32_t)(m & 1) << 15);
+            const int l = j / M, rr = j % M;
+            const int tid = (l / spw) * 64 + rr / eps, i = (l % spw) * eps + rr % eps;
+            pos2[((size_t)t * (J / 2) + i / 2) * T + tid] |= lds << (16 * (i & 1));
+        }
+        std::vector<std::vector<std::pair<int, cd>>> gcon(N2);
+        for (int i = 0; i < Mr; ++i) {
+            long long a, b;
+            cd c1, c2;
+            fwd_coef(o0[i], N, N2, t_scale[t], &a, &b, &c1, &c2);
+            oab[(size_t)t * Mr + i] = (uint32_t)(a % 4096) | ((uint32_t)(b % 4096) << 16);
+            for (int m2 = 0; m2 < 2; ++m2)
+                for (int r = 0; r < 4; ++r) {
+                    cd *o = &oc[(((size_t)t * 2 + m2) * Mr + i) * 8];
+                    o[r] = c1 * tw((long long)(m2 + 2 * r) * a, N2);
+                    o[4 + r] = c2 * std::conj(tw((long long)(m2 + 2 * r) * b, N2));
+                }
+            inv_contrib(o0[i], N, N2, t_scale[t], [&](long long k, cd c) { gcon[k].push_back({i, c}); });
+        }
+        for (int k = 0; k < N2; ++k) {
+            if (gcon[k].empty()) continue;
+            SG_CHECK_ARG(gcon[k].size() <= 4, "internal: >4 contributions to one G slot");
+            gk.push_back(k);
+            gloc.push_back((uint16_t)fsw(k & (int)(N2 / 2 - 1)));
+            grow.push_back(row_of[t]);
+            for (int q = 0; q < 4; ++q) {
+                if (q < (int)gcon[k].size()) { gi.push_back(gcon[k][q].first); gc.push_back(gcon[k][q].second); }
+                else { gi.push_back(-1); gc.push_back(cd(0, 0)); }
+            }
+        }
+        gptr[t + 1] = (int32_t)gk.size();
+    }
+    std::vector<cd> stw;  // stage twiddles of the P-point FFT (fft.hpp lds_fft1_ct, EPT 16)
+    {
+        int radix[8];
+        const int ns = fft1_plan(14, 16, radix);
+        int lns = 0;
+        for (int st = 0; st < ns; ++st) {
+            const int R = radix[st];
+            const long long Ns = 1LL << lns;
+            for (long long k = 0; k < Ns; ++k)
+                for (int q = 0; q < tw_per_k(R); ++q) stw.push_back(tw(tw_exp(R, q) * k, Ns * R));
+            lns += ilog2(R);
+        }
+    }
+    SG_TRY(upload(p, &p->b_pos2, pos2));
+    SG_TRY(upload(p, &p->b_oab, oab));
+    SG_TRY(upload_cx(p, &p->b_oc, oc));
+    SG_TRY(upload(p, &p->b_gptr, gptr));
+    SG_TRY(upload(p, &p->b_grow, grow));
+    p->b_ngs = gptr[nT];
+    SG_TRY(upload(p, &p->b_gloc, gloc));
+    SG_TRY(upload(p, &p->b_gk, gk));
+    SG_TRY(upload(p, &p->b_gi, gi));
+    SG_TRY(upload_cx(p, &p->b_gc, gc));
+    SG_TRY(upload_cx(p, &p->b_stw, stw));
+    SG_CHECK_ARG(blk2_lds_bytes() <= 160 * 1024, "block engine LDS budget");
+    return SG_OK;
+}
+
 static int build_plan(int ndim, const double *W, int Lr_in, int Lc_in, int L, int M, int n, const uint32_t *order0,
                       const uint32_t *order1, int precision, bool no_cw, sg_amp_plan **out) {
     SG_CHECK_ARG(out && W && order0 && order1, "null argument");
@@ -820,6 +904,10 @@ static int build_plan(int ndim, const double *W, int Lr_in, int Lc_in, int L, in
     // workgroup's LDS: the block engine (single precision, w = 2^15)
     p->block = !p->regular && precision == SG_F32 && p->N2 == (1 << 14) && Mc == (1 << 14) && M >= 64 &&
                M <= 1024 && Mr < 65536 && !(eng && (std::strcmp(eng, "legacy") == 0 || std::strcmp(eng, "general") == 0));
+    // w = 2^16 with Mc = 2^15 (the notebook geometry): the two-class form
+    p->block2 = !p->regular && !p->block && precision == SG_F32 && p->N2 == (1 << 15) && Mc == (1 << 15) &&
+                M >= 64 && M <= 2048 && Mr <= 1024 &&
+                !(eng && (std::strcmp(eng, "legacy") == 0 || std::strcmp(eng, "general") == 0));
     const int N = w, N2 = p->N2, P = p->P, Q = p->Q, np1 = p->npairs + 1;
     auto slot_of = [&](long long pos) -> long long {  // w-space slot of position pos
         return (pos % 2 == 0) ? pos / 2 : (long long)N - 1 - (pos - 1) / 2;
@@ -927,6 +1015,7 @@ static int build_plan(int ndim, const double *W, int Lr_in, int Lc_in, int L, in
     SG_TRY(upload(pp, &pp->dW, Wd));
     if (pp->regular) SG_TRY(build_regular(pp, order0, order1, t_scale));
     if (pp->block) SG_TRY(build_block(pp, order0, order1, t_scale, t_row));
+    if (pp->block2) SG_TRY(build_block2(pp, order0, order1, t_scale, t_row));
     return SG_OK;
     }();
     if (rc != SG_OK) {
@@ -1023,16 +1112,17 @@ static int decode_impl(sg_amp_plan *p, const void *d_y, int B, const int32_t *d_
     SG_HIP(hipMemsetAsync(p->ws_beta, 0, (size_t)B * p->LM * rs, s));
     SG_TRY(amp_launch_control<T>(tb, bf, sc, pr, 2, 0, s));
     std::vector<int32_t> act(B);
-    const bool blk = p->block && sizeof(T) == 4;
+    const bool blk = (p->block || p->block2) && sizeof(T) == 4;
     const BlkTables bt = blk ? btables(p) : BlkTables{};
     p->last_engine = blk ? 3 : 0;
     p->last_handover = -1;
     for (int t = 0; t < t_max - 1; ++t) {
         if constexpr (sizeof(T) == 4) {
             if (blk) {
-                if (t > 0) SG_TRY(blk_launch_ab(bt, bf, s));
+                if (t > 0) SG_TRY(p->block2 ? blk2_launch_ab(bt, bf, s) : blk_launch_ab(bt, bf, s));
                 SG_TRY(amp_launch_control<T>(tb, bf, sc, pr, 0, t, s));
-                SG_TRY(blk_launch_az(bt, bf, (cx<float> *)p->ws_gbuf, s));
+                SG_TRY(p->block2 ? blk2_launch_az(bt, bf, (cx<float> *)p->ws_gbuf, s)
+                                 : blk_launch_az(bt, bf, (cx<float> *)p->ws_gbuf, s));
                 SG_TRY(amp_launch_control<T>(tb, bf, sc, pr, 1, t, s));
             }
         }
@@ -1187,7 +1277,7 @@ int sg_amp_plan_destroy(sg_amp_plan *p) {
 int sg_amp_plan_engine(const sg_amp_plan *p, int B) {
     SG_CHECK_ARG(p, "plan is NULL");
     if (p->regular) return (p->precision == SG_F32 && sg::use_cw(p, B)) ? 2 : 1;
-    return p->block ? 3 : 0;
+    return (p->block || p->block2) ? 3 : 0;
 }
 
 int sg_amp_last_decode(const sg_amp_plan *p, int *engine, int *handover_iter, int *on_companion) {

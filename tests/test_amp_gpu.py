@@ -274,7 +274,8 @@ def _notebook_design(seed):
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 def test_notebook_geometry_vs_oracle(precision):
     """The reference's only published M=512 configuration, one codeword of the
-    notebook's geometry against the CPU restatement of sparc.py:883-999:
+    notebook's geometry against the CPU restatement of sparc.py:883-999 (f32
+    through the two-class block engine, f64 through the general path):
     f64 -- same t_final and MAP decisions, NMSE within 1e-9; f32 -- t_final
     within 2, decisions on all but 0.5 % of the sections, NMSE within 2e-3
     over the first 10 iterations."""
@@ -282,7 +283,8 @@ def test_notebook_geometry_vs_oracle(precision):
     op = sparc.DesignOperator(W, L, M, n, o0, o1)
     assert op.w == 2 ** 16 and W.shape == (37, 32) and n == 12284
     prec = _native.SG_F64 if precision == "f64" else _native.SG_F32
-    assert _native.lib().sg_amp_plan_engine(op.plan(prec), 1) == 0  # the general path
+    # f32: the two-class block engine (amp_block2.hip); f64: the general path
+    assert _native.lib().sg_amp_plan_engine(op.plan(prec), 1) == (3 if precision == "f32" else 0)
     Ab, Az = sparc_ref.dct_operators(W, L, M, n, o0, o1)
     rng = np.random.RandomState(14)
     true = rng.randint(0, M, L)
@@ -302,6 +304,44 @@ def test_notebook_geometry_vs_oracle(precision):
         assert np.mean(mi[0] != ref_map) < 0.005
         np.testing.assert_allclose(nm[0, :10], rn[:10], atol=2e-3)
     assert np.mean(ref_map != true) < 0.01  # the decode wave runs through at this size
+
+
+def test_notebook_block2_vs_general_engine(monkeypatch):
+    """The two-class block engine (amp_block2.hip) and the general four-step
+    engine (SG_AMP_ENGINE=general) decode the same batch of the notebook's
+    geometry to the same decisions and stopping iterations (f32)."""
+    W, L, M, n, o0, o1 = _notebook_design(17)
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    Y, true = _c4_batch(op, 8, 19)
+    monkeypatch.delenv("SG_AMP_ENGINE", raising=False)
+    mb, tb_, nb, _ = sparc.amp_decode_batch(Y, op, 1.0, 40, true_idx=true, precision=_native.SG_F32)
+    assert _native.amp_last_decode(op.plan(_native.SG_F32))["engine"] == 3
+    monkeypatch.setenv("SG_AMP_ENGINE", "general")
+    og = sparc.DesignOperator(W, L, M, n, o0, o1)
+    mg, tg, ng, _ = sparc.amp_decode_batch(Y, og, 1.0, 40, true_idx=true, precision=_native.SG_F32)
+    assert _native.amp_last_decode(og.plan(_native.SG_F32))["engine"] == 0
+    assert np.all(np.abs(tb_ - tg) <= 1)
+    assert np.mean(mb != mg) < 1e-3
+    np.testing.assert_allclose(nb[:, :10], ng[:, :10], atol=1e-4)
+    assert np.mean(mb != true) < 0.01
+
+
+def test_notebook_block2_operators():
+    """The two-class block engine's forward and adjoint operators (through
+    decoding-free applications would need the general plan; here: one AMP
+    iteration pair) -- checked through the first NMSE value, which depends only
+    on Ab and Az of the first iteration, against the CPU restatement."""
+    W, L, M, n, o0, o1 = _notebook_design(21)
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    Ab, Az = sparc_ref.dct_operators(W, L, M, n, o0, o1)
+    rng = np.random.RandomState(22)
+    true = rng.randint(0, M, L)
+    beta0 = np.zeros(L * M)
+    beta0[np.arange(L) * M + true] = 1
+    y = Ab(beta0) + rng.randn(n)
+    rb, rt, rn, rp = sparc_ref.amp(y, W, L, M, n, 1.0, 3, Ab, Az, beta0)
+    mi, tf, nm, ps = sparc.amp_decode_batch(y[None], op, 1.0, 3, true_idx=true[None], precision=_native.SG_F32)
+    np.testing.assert_allclose(nm[0], np.asarray(rn).reshape(3, -1), atol=2e-4)
 
 
 # ---- per-codeword engine (amp_cw.hip): opt-in with SG_AMP_ENGINE=cw (plan
