@@ -27,6 +27,21 @@ template <typename T>
 __device__ __forceinline__ cx<T> cmul(cx<T> a, cx<T> b) {
     return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x};
 }
+// Single precision: the product in two packed instructions, t = (a.y b.y,
+// a.y b.x) by v_pk_mul_f32, then (a.x b.x - t.x, a.x b.y + t.y) by one
+// v_pk_fma_f32 with the low product negated.  The compiler's own lowering of
+// the scalar form takes three to six instructions; in the 8192-point LDS FFT
+// of the per-codeword engine this takes the stage-twiddle cost from 4.5 k to
+// 2.0 k cycles per transform (tools/fftbench variant 5).
+typedef float sg_f2 __attribute__((ext_vector_type(2)));
+template <>
+__device__ __forceinline__ cx<float> cmul<float>(cx<float> a, cx<float> b) {
+    const sg_f2 A = {a.x, a.y}, Bv = {b.x, b.y};
+    sg_f2 t, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0]" : "=v"(t) : "v"(A), "v"(Bv));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_lo:[0,0,1]" : "=v"(r) : "v"(A), "v"(Bv), "v"(t));
+    return {r.x, r.y};
+}
 template <typename T>
 __device__ __forceinline__ cx<T> cconj(cx<T> a) { return {a.x, -a.y}; }
 // multiply by -i (forward) or +i (inverse)

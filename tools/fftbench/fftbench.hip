@@ -22,6 +22,30 @@ __device__ __forceinline__ int opaque(int v) {
     return v;
 }
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+// complex product in two packed instructions (v_pk_mul_f32 + v_pk_fma_f32)
+__device__ __forceinline__ cx<float> cmul_pk(cx<float> a, cx<float> b) {
+    f2v A = {a.x, a.y}, Bv = {b.x, b.y}, t, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0]" : "=v"(t) : "v"(A), "v"(Bv));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_lo:[0,0,1]" : "=v"(r) : "v"(A), "v"(Bv), "v"(t));
+    return {r.x, r.y};
+}
+template <bool INV>
+__device__ __forceinline__ void tw_apply8_pk(const cx<float> *wl, cx<float> *v) {
+    cx<float> a[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) a[t] = INV ? cconj(wl[t]) : wl[t];
+#pragma unroll
+    for (int b = 1; b < 4; ++b) v[b] = cmul_pk(v[b], a[b - 1]);
+    v[4] = cmul_pk(v[4], a[3]);
+#pragma unroll
+    for (int b = 1; b < 4; ++b) v[4 + b] = cmul_pk(v[4 + b], cmul_pk(a[3], a[b - 1]));
+}
+template <bool INV>
+__device__ __forceinline__ void tw_apply2_pk(const cx<float> *wl, cx<float> *v) {
+    v[1] = cmul_pk(v[1], INV ? cconj(wl[0]) : wl[0]);
+}
+
 constexpr int radix(int st) { return st < 4 ? 8 : 2; }
 constexpr int log2ns(int st) {
     int l = 0;
@@ -30,7 +54,7 @@ constexpr int log2ns(int st) {
 }
 
 // one Stockham stage from src to dst (src == dst: two barriers)
-template <bool INV, int ST, bool PP, bool TW = true, bool DFT = true>
+template <bool INV, int ST, bool PP, bool TW = true, bool DFT = true, bool PK = false>
 __device__ __forceinline__ void stage(const cx<float> *src, cx<float> *dst, int tid) {
     constexpr int R = radix(ST), LNS = log2ns(ST), NB = EPT / R, TWN = tw_per_k(R);
     constexpr int LR = R == 2 ? 1 : 3;
@@ -57,7 +81,11 @@ __device__ __forceinline__ void stage(const cx<float> *src, cx<float> *dst, int 
         const int jp = fsw(j);
 #pragma unroll
         for (int r = 0; r < R; ++r) v[i * R + r] = src[(NBF % 256 == 0) ? jp + r * NBF : fsw(j + r * NBF)];
-        if constexpr (LNS > 0 && TW) tw_apply<float, INV, R>(wl + i * TWN, &v[i * R]);
+        if constexpr (LNS > 0 && TW) {
+            if constexpr (PK && R == 8) tw_apply8_pk<INV>(wl + i * TWN, &v[i * R]);
+            else if constexpr (PK && R == 2) tw_apply2_pk<INV>(wl + i * TWN, &v[i * R]);
+            else tw_apply<float, INV, R>(wl + i * TWN, &v[i * R]);
+        }
         if constexpr (DFT) dftR<float, INV, R>(&v[i * R]);
         base_out[i] = ((j - k) << LR) + k;
     }
@@ -257,6 +285,12 @@ __global__ __launch_bounds__(T) void bench(float *out, long long *cyc, int nf) {
             stage<false, 2, false, false, false>(A, A, tl);
             stage<false, 3, false, false, false>(A, A, tl);
             stage<false, 4, false, false, false>(A, A, tl);
+        } else if constexpr (VAR == 5) {  // packed complex products (inline asm)
+            stage<false, 0, false, true, true, true>(A, A, tl);
+            stage<false, 1, false, true, true, true>(A, A, tl);
+            stage<false, 2, false, true, true, true>(A, A, tl);
+            stage<false, 3, false, true, true, true>(A, A, tl);
+            stage<false, 4, false, true, true, true>(A, A, tl);
         } else if constexpr (VAR == 4) {  // two transforms per pass (counted as two)
             if (f & 1) continue;
             stage2<false, 0>(A, Bf, tl);
@@ -313,6 +347,7 @@ int main() {
     run<2>(nb, nf);
     run<3>(nb, nf);
     run<4>(nb, nf);
+    run<5>(nb, nf);
     grun<1024, 8, 0, false>("g1024x8 r8 2bar", nb, nf);
     grun<512, 16, 0, false>("g512x16 r8 2bar", nb, nf);
     grun<512, 16, 0, true>("g512x16 r8 pingpong", nb, nf);
