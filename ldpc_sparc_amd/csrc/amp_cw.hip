@@ -193,8 +193,7 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
                 for (int j = 0; j < KT; ++j) {  // invalid slots accumulate into themselves, unused
                     const cx<float> Tv = d[fsw(kt[j] & (CW_P - 1))];
                     cx<float> x = j < CW_KL ? Xl[j * CW_THREADS + tl] : Xr[j < CW_KL ? 0 : j - CW_KL];
-                    x.x += Tv.x * w[j].x - Tv.y * w[j].y;
-                    x.y += Tv.x * w[j].y + Tv.y * w[j].x;
+                    x = cmac_pk(x, Tv, w[j]);
                     if (j < CW_KL) Xl[j * CW_THREADS + tl] = x;
                     else Xr[j < CW_KL ? 0 : j - CW_KL] = x;
                 }
@@ -378,8 +377,7 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
                 if (!(kt[j] & CW_VALID)) continue;
                 const cx<float> gv = j < CW_KL ? Xl[j * CW_THREADS + tl] : Xr[j < CW_KL ? 0 : j - CW_KL];
                 if (kt[j] & CW_NEWROW) u = {0.f, 0.f};
-                u.x += gv.x * w[j].x + gv.y * w[j].y;  // G conj(w_N2^(m2 k))
-                u.y += gv.y * w[j].x - gv.x * w[j].y;
+                u = cmacc_pk(u, gv, w[j]);  // G conj(w_N2^(m2 k))
                 if (kt[j] & CW_ENDROW) d[fsw(kt[j] & (CW_P - 1))] = u;
             }
         }

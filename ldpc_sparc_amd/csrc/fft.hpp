@@ -42,6 +42,23 @@ __device__ __forceinline__ cx<float> cmul<float>(cx<float> a, cx<float> b) {
     asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_lo:[0,0,1]" : "=v"(r) : "v"(A), "v"(Bv), "v"(t));
     return {r.x, r.y};
 }
+// x + a b and x + a conj(b) in two packed FMAs (single precision)
+__device__ __forceinline__ cx<float> cmac_pk(cx<float> x, cx<float> a, cx<float> b) {
+    const sg_f2 X = {x.x, x.y}, A = {a.x, a.y}, Bv = {b.x, b.y};
+    sg_f2 t, r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(t) : "v"(A), "v"(Bv), "v"(X));  // x + a.x b
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"
+        : "=v"(r) : "v"(A), "v"(Bv), "v"(t));  // + (-a.y b.y, a.y b.x)
+    return {r.x, r.y};
+}
+__device__ __forceinline__ cx<float> cmacc_pk(cx<float> x, cx<float> a, cx<float> b) {
+    const sg_f2 X = {x.x, x.y}, A = {a.x, a.y}, Bv = {b.x, b.y};
+    sg_f2 t, r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(t) : "v"(A), "v"(Bv), "v"(X));  // x + a b.x
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]"
+        : "=v"(r) : "v"(A), "v"(Bv), "v"(t));  // + (a.y b.y, -a.x b.y)
+    return {r.x, r.y};
+}
 template <typename T>
 __device__ __forceinline__ cx<T> cconj(cx<T> a) { return {a.x, -a.y}; }
 // multiply by -i (forward) or +i (inverse)
