@@ -27,36 +27,35 @@ template <typename T>
 __device__ __forceinline__ cx<T> cmul(cx<T> a, cx<T> b) {
     return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x};
 }
-// Single precision: the product in two packed instructions, t = (a.y b.y,
-// a.y b.x) by v_pk_mul_f32, then (a.x b.x - t.x, a.x b.y + t.y) by one
-// v_pk_fma_f32 with the low product negated.  The compiler's own lowering of
-// the scalar form takes three to six instructions; in the 8192-point LDS FFT
-// of the per-codeword engine this takes the stage-twiddle cost from 4.5 k to
-// 2.0 k cycles per transform (tools/fftbench variant 5).
+// Single precision: the product in two packed instructions, t = a.x (b.x, b.y)
+// by v_pk_mul_f32, then t + (-a.y b.y, a.y b.x) by one v_pk_fma_f32 whose
+// operand swizzles and lane negation the compiler folds into op_sel / neg_lo.
+// The scalar form lowers to three to six instructions; in the 8192-point LDS
+// FFT of the per-codeword engine this takes the stage-twiddle cost from 4.5 k
+// to 2.0 k cycles per transform (tools/fftbench variant 5).  Written as vector
+// arithmetic, not inline assembly: the compiler's hazard recognizer must see
+// the operands (a v_pk op reading a v_sin_f32 result in the next instruction
+// needs a wait state that it does not insert for an asm block -- measured
+// wrong in tools/fftbench's accuracy check).
 typedef float sg_f2 __attribute__((ext_vector_type(2)));
 template <>
 __device__ __forceinline__ cx<float> cmul<float>(cx<float> a, cx<float> b) {
-    const sg_f2 A = {a.x, a.y}, Bv = {b.x, b.y};
-    sg_f2 t, r;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0]" : "=v"(t) : "v"(A), "v"(Bv));
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_lo:[0,0,1]" : "=v"(r) : "v"(A), "v"(Bv), "v"(t));
+    const sg_f2 A = {a.x, a.y}, B = {b.x, b.y};
+    const sg_f2 an = {-a.y, a.y};
+    const sg_f2 r = __builtin_elementwise_fma(an, B.yx, A.xx * B);
     return {r.x, r.y};
 }
 // x + a b and x + a conj(b) in two packed FMAs (single precision)
 __device__ __forceinline__ cx<float> cmac_pk(cx<float> x, cx<float> a, cx<float> b) {
-    const sg_f2 X = {x.x, x.y}, A = {a.x, a.y}, Bv = {b.x, b.y};
-    sg_f2 t, r;
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(t) : "v"(A), "v"(Bv), "v"(X));  // x + a.x b
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"
-        : "=v"(r) : "v"(A), "v"(Bv), "v"(t));  // + (-a.y b.y, a.y b.x)
+    const sg_f2 X = {x.x, x.y}, A = {a.x, a.y}, B = {b.x, b.y};
+    const sg_f2 an = {-a.y, a.y};
+    const sg_f2 r = __builtin_elementwise_fma(an, B.yx, __builtin_elementwise_fma(A.xx, B, X));
     return {r.x, r.y};
 }
 __device__ __forceinline__ cx<float> cmacc_pk(cx<float> x, cx<float> a, cx<float> b) {
-    const sg_f2 X = {x.x, x.y}, A = {a.x, a.y}, Bv = {b.x, b.y};
-    sg_f2 t, r;
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(t) : "v"(A), "v"(Bv), "v"(X));  // x + a b.x
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]"
-        : "=v"(r) : "v"(A), "v"(Bv), "v"(t));  // + (a.y b.y, -a.x b.y)
+    const sg_f2 X = {x.x, x.y}, A = {a.x, a.y}, B = {b.x, b.y};
+    const sg_f2 an = {a.y, -a.x};
+    const sg_f2 r = __builtin_elementwise_fma(an, B.yy, __builtin_elementwise_fma(A, B.xx, X));
     return {r.x, r.y};
 }
 template <typename T>

@@ -5,9 +5,14 @@
 //   0  amp_cw.hip's stage schedule: radix 8,8,8,8,2, twiddles from the
 //      hardware sine/cosine, one image, two barriers per stage
 //   1  ping-pong between two images: one barrier per stage
+//   2  no twiddles; 3  no twiddles and no butterflies (LDS traffic and barriers)
+//   4  two transforms through the same barriers; 5  packed complex products
+//   6, 7  as 5 with 1 or 2 sine/cosine pairs per radix-8 butterfly (the other
+//         powers of w as packed products) instead of 4
 // Build: hipcc -O3 --offload-arch=gfx950 -I../../ldpc_sparc_amd/csrc fftbench.hip -o fftbench
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdio>
 #include <vector>
 
@@ -22,13 +27,10 @@ __device__ __forceinline__ int opaque(int v) {
     return v;
 }
 
-typedef float f2v __attribute__((ext_vector_type(2)));
-// complex product in two packed instructions (v_pk_mul_f32 + v_pk_fma_f32)
-__device__ __forceinline__ cx<float> cmul_pk(cx<float> a, cx<float> b) {
-    f2v A = {a.x, a.y}, Bv = {b.x, b.y}, t, r;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0]" : "=v"(t) : "v"(A), "v"(Bv));
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_lo:[0,0,1]" : "=v"(r) : "v"(A), "v"(Bv), "v"(t));
-    return {r.x, r.y};
+// complex product in two packed instructions (fft.hpp's cmul<float>)
+__device__ __forceinline__ cx<float> cmul_pk(cx<float> a, cx<float> b) { return cmul(a, b); }
+__device__ __forceinline__ cx<float> csq(cx<float> a) {
+    return {a.x * a.x - a.y * a.y, 2.f * a.x * a.y};
 }
 template <bool INV>
 __device__ __forceinline__ void tw_apply8_pk(const cx<float> *wl, cx<float> *v) {
@@ -54,7 +56,7 @@ constexpr int log2ns(int st) {
 }
 
 // one Stockham stage from src to dst (src == dst: two barriers)
-template <bool INV, int ST, bool PP, bool TW = true, bool DFT = true, bool PK = false>
+template <bool INV, int ST, bool PP, bool TW = true, bool DFT = true, bool PK = false, int NTR = 4>
 __device__ __forceinline__ void stage(const cx<float> *src, cx<float> *dst, int tid) {
     constexpr int R = radix(ST), LNS = log2ns(ST), NB = EPT / R, TWN = tw_per_k(R);
     constexpr int LR = R == 2 ? 1 : 3;
@@ -67,8 +69,17 @@ __device__ __forceinline__ void stage(const cx<float> *src, cx<float> *dst, int 
             const int k = (tid + i * T) & (NS - 1);
 #pragma unroll
             for (int q = 0; q < TWN; ++q) {
+                if (R == 8 && q >= NTR) continue;
                 const float x = (float)((tw_exp(R, q) * k) & ((1 << (LNS + LR)) - 1)) * inv;
                 wl[i * TWN + q] = {__builtin_amdgcn_cosf(x), -__builtin_amdgcn_sinf(x)};
+            }
+            if constexpr (R == 8 && NTR == 1) {  // w^2, w^3, w^4 as products of w
+                wl[i * TWN + 1] = csq(wl[i * TWN]);
+                wl[i * TWN + 2] = cmul_pk(wl[i * TWN], wl[i * TWN + 1]);
+                wl[i * TWN + 3] = csq(wl[i * TWN + 1]);
+            } else if constexpr (R == 8 && NTR == 2) {  // w^3 = w w^2, w^4 = w^2 w^2
+                wl[i * TWN + 2] = cmul_pk(wl[i * TWN], wl[i * TWN + 1]);
+                wl[i * TWN + 3] = csq(wl[i * TWN + 1]);
             }
         }
     }
@@ -291,6 +302,13 @@ __global__ __launch_bounds__(T) void bench(float *out, long long *cyc, int nf) {
             stage<false, 2, false, true, true, true>(A, A, tl);
             stage<false, 3, false, true, true, true>(A, A, tl);
             stage<false, 4, false, true, true, true>(A, A, tl);
+        } else if constexpr (VAR == 6 || VAR == 7) {  // packed, 1 (6) or 2 (7) sine/cosine pairs per radix-8 butterfly
+            constexpr int NT = VAR == 6 ? 1 : 2;
+            stage<false, 0, false, true, true, true, NT>(A, A, tl);
+            stage<false, 1, false, true, true, true, NT>(A, A, tl);
+            stage<false, 2, false, true, true, true, NT>(A, A, tl);
+            stage<false, 3, false, true, true, true, NT>(A, A, tl);
+            stage<false, 4, false, true, true, true, NT>(A, A, tl);
         } else if constexpr (VAR == 4) {  // two transforms per pass (counted as two)
             if (f & 1) continue;
             stage2<false, 0>(A, Bf, tl);
@@ -340,14 +358,67 @@ static double run(int nb, int nf) {
     return s / nb / nf;
 }
 
+// one forward transform of a fixed input per NTR setting, written out (accuracy check of variants 5-7)
+template <int NT>
+__global__ __launch_bounds__(T) void check_fft(float2 *out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cx<float> *A = reinterpret_cast<cx<float> *>(smem);
+    const int tid = threadIdx.x;
+    for (int i = tid; i < P; i += T) A[fsw(i)] = {(float)((i * 37) % 101) / 101.f - 0.5f, (float)((i * i) % 97) / 97.f - 0.5f};
+    __syncthreads();
+    stage<false, 0, false, true, true, true, NT>(A, A, tid);
+    stage<false, 1, false, true, true, true, NT>(A, A, tid);
+    stage<false, 2, false, true, true, true, NT>(A, A, tid);
+    stage<false, 3, false, true, true, true, NT>(A, A, tid);
+    stage<false, 4, false, true, true, true, NT>(A, A, tid);
+    for (int i = tid; i < P; i += T) out[i] = make_float2(A[fsw(i)].x, A[fsw(i)].y);
+}
+template <int NT>
+static std::vector<float2> check(void) {
+    float2 *o;
+    hipMalloc(&o, sizeof(float2) * P);
+    hipFuncSetAttribute((const void *)check_fft<NT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipLaunchKernelGGL(check_fft<NT>, dim3(1), dim3(T), 160 * 1024, 0, o);
+    std::vector<float2> h(P);
+    hipMemcpy(h.data(), o, sizeof(float2) * P, hipMemcpyDeviceToHost);
+    hipFree(o);
+    return h;
+}
+
 int main() {
     const int nb = 256, nf = 256;
+    {
+        // reference: direct DFT in double of the same input
+        std::vector<double> xr(P), xi(P);
+        for (int i = 0; i < P; ++i) {
+            xr[i] = (float)((i * 37) % 101) / 101.f - 0.5f;
+            xi[i] = (float)(((long long)i * i) % 97) / 97.f - 0.5f;
+        }
+        auto a4 = check<4>(), a2 = check<2>(), a1 = check<1>();
+        double e4 = 0, e2 = 0, e1 = 0, nrm = 0;
+        for (int k = 0; k < P; k += 61) {
+            double sr = 0, si = 0;
+            for (int m = 0; m < P; ++m) {
+                const double ang = -2 * M_PI * (double)((long long)m * k % P) / P;
+                sr += xr[m] * cos(ang) - xi[m] * sin(ang);
+                si += xr[m] * sin(ang) + xi[m] * cos(ang);
+            }
+            nrm = fmax(nrm, hypot(sr, si));
+            e4 = fmax(e4, hypot(a4[k].x - sr, a4[k].y - si));
+            e2 = fmax(e2, hypot(a2[k].x - sr, a2[k].y - si));
+            e1 = fmax(e1, hypot(a1[k].x - sr, a1[k].y - si));
+        }
+        printf("accuracy (max abs error / max |X|): 4 sincos %.3g, 2 sincos %.3g, 1 sincos %.3g\n", e4 / nrm, e2 / nrm,
+               e1 / nrm);
+    }
     run<0>(nb, nf);
     run<1>(nb, nf);
     run<2>(nb, nf);
     run<3>(nb, nf);
     run<4>(nb, nf);
     run<5>(nb, nf);
+    run<6>(nb, nf);
+    run<7>(nb, nf);
     grun<1024, 8, 0, false>("g1024x8 r8 2bar", nb, nf);
     grun<512, 16, 0, false>("g512x16 r8 2bar", nb, nf);
     grun<512, 16, 0, true>("g512x16 r8 pingpong", nb, nf);
