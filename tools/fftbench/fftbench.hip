@@ -9,7 +9,10 @@
 //   4  two transforms through the same barriers; 5  packed complex products
 //   6, 7  as 5 with 1 or 2 sine/cosine pairs per radix-8 butterfly (the other
 //         powers of w as packed products) instead of 4
-// Build: hipcc -O3 --offload-arch=gfx950 -I../../ldpc_sparc_amd/csrc fftbench.hip -o fftbench
+//   8  wfft.hpp: 16 x 512 four-step, one workgroup exchange, the 512-point
+//      sub-transforms inside each wavefront (two workgroup barriers)
+// and an accuracy check of variants 5-8 against a double-precision DFT
+// Build: hipcc -O3 --offload-arch=gfx950 -I../../ldpc_sparc_amd/csrc -I. fftbench.hip -o fftbench
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -17,6 +20,7 @@
 #include <vector>
 
 #include "fft.hpp"
+#include "wfft.hpp"
 
 using namespace sg;
 
@@ -309,6 +313,8 @@ __global__ __launch_bounds__(T) void bench(float *out, long long *cyc, int nf) {
             stage<false, 2, false, true, true, true, NT>(A, A, tl);
             stage<false, 3, false, true, true, true, NT>(A, A, tl);
             stage<false, 4, false, true, true, true, NT>(A, A, tl);
+        } else if constexpr (VAR == 8) {  // wfft.hpp: 16 x 512 with one workgroup exchange
+            wfft8192<false>(A, tl);
         } else if constexpr (VAR == 4) {  // two transforms per pass (counted as two)
             if (f & 1) continue;
             stage2<false, 0>(A, Bf, tl);
@@ -385,8 +391,53 @@ static std::vector<float2> check(void) {
     return h;
 }
 
+template <bool INV>
+__global__ __launch_bounds__(T) void check_wfft(float2 *out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cx<float> *A = reinterpret_cast<cx<float> *>(smem);
+    const int tid = threadIdx.x;
+    for (int i = tid; i < P; i += T) A[i] = {(float)((i * 37) % 101) / 101.f - 0.5f, (float)((i * i) % 97) / 97.f - 0.5f};
+    __syncthreads();
+    wfft8192<INV>(A, tid);
+    for (int k = tid; k < P; k += T) out[k] = make_float2(A[wf_pos_out(k)].x, A[wf_pos_out(k)].y);
+}
+template <bool INV>
+static std::vector<float2> checkw(void) {
+    float2 *o;
+    hipMalloc(&o, sizeof(float2) * P);
+    hipFuncSetAttribute((const void *)check_wfft<INV>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipLaunchKernelGGL(check_wfft<INV>, dim3(1), dim3(T), 160 * 1024, 0, o);
+    std::vector<float2> h(P);
+    hipMemcpy(h.data(), o, sizeof(float2) * P, hipMemcpyDeviceToHost);
+    hipFree(o);
+    return h;
+}
+
 int main() {
     const int nb = 256, nf = 256;
+    {
+        std::vector<double> xr(P), xi(P);
+        for (int i = 0; i < P; ++i) {
+            xr[i] = (float)((i * 37) % 101) / 101.f - 0.5f;
+            xi[i] = (float)(((long long)i * i) % 97) / 97.f - 0.5f;
+        }
+        auto f = checkw<false>(), g = checkw<true>();
+        double ef = 0, eg = 0, nrm = 0;
+        for (int k = 0; k < P; k += 13) {
+            double sr = 0, si = 0, tr = 0, ti = 0;
+            for (int m = 0; m < P; ++m) {
+                const double ang = -2 * M_PI * (double)((long long)m * k % P) / P;
+                sr += xr[m] * cos(ang) - xi[m] * sin(ang);
+                si += xr[m] * sin(ang) + xi[m] * cos(ang);
+                tr += xr[m] * cos(ang) + xi[m] * sin(ang);
+                ti += -xr[m] * sin(ang) + xi[m] * cos(ang);
+            }
+            nrm = fmax(nrm, hypot(sr, si));
+            ef = fmax(ef, hypot(f[k].x - sr, f[k].y - si));
+            eg = fmax(eg, hypot(g[k].x - tr, g[k].y - ti));
+        }
+        printf("wfft accuracy (max abs error / max |X|): forward %.3g, inverse %.3g\n", ef / nrm, eg / nrm);
+    }
     {
         // reference: direct DFT in double of the same input
         std::vector<double> xr(P), xi(P);
@@ -419,6 +470,7 @@ int main() {
     run<5>(nb, nf);
     run<6>(nb, nf);
     run<7>(nb, nf);
+    run<8>(nb, nf);
     grun<1024, 8, 0, false>("g1024x8 r8 2bar", nb, nf);
     grun<512, 16, 0, false>("g512x16 r8 2bar", nb, nf);
     grun<512, 16, 0, true>("g512x16 r8 pingpong", nb, nf);
