@@ -518,7 +518,7 @@ def sc_bench(args, d, comm, cpu_seconds, procs, L=1024, B=None, steps=None, seed
     cw_it = int(tf.sum()) * steps
     kms = sum(ph.get(k, (0.0, 0))[0] for k in AMP_PHASES)
     w = int(op.w)
-    sc_traffic, sc_tfile = pmc_traffic("sc", "hbm_bytes_per_codeword_iteration_approx")
+    sc_traffic, sc_tfile = pmc_traffic("sc" if L == 1024 else "sc_notebook", "hbm_bytes_per_codeword_iteration")
     flops = 2 * int(np.count_nonzero(W)) * 2.5 * w * np.log2(w) + 20 * L * M  # per codeword-iteration
     ach = flops * cw_it / (kms * 1e-3) / 1e12 if kms else None
     out = {"workload": f"spatially coupled SPARC (omega=6, Lambda=32, W 37x32, 192 transforms of w=2^{int(np.log2(w))}), "
@@ -530,12 +530,13 @@ def sc_bench(args, d, comm, cpu_seconds, procs, L=1024, B=None, steps=None, seed
            "roofline": {"bound": "valu-f32", "achieved": ach, "peak": VALU_PEAK_TFS, "unit": "TFLOP/s",
                         "frac": ach / VALU_PEAK_TFS if ach else None,
                         "traffic": sc_traffic,
-                        "traffic_unit": "HBM bytes per codeword-iteration, block-engine kernels (PMC, "
-                                        f"profiles/{sc_tfile})",
+                        "traffic_unit": "HBM bytes per executed codeword-iteration: every dispatch of the "
+                                        f"engine's decodes (PMC, profiles/{sc_tfile})",
                         "kernel": ("blk2_ab + blk_g + blk2_az + control (amp_block2.hip)" if "two-class" in engine else
                                    "blk_ab + blk_g + blk_az + control (amp_block.hip)") if "block" in engine else
                                   "general four-step kernels (amp_dct.hip)",
                         "algorithmic_flops_per_codeword_iteration": flops,
+                        "algorithmic_bytes_per_codeword_iteration": 4 * (2 * L * M + 4 * n),
                         "note": "2 nT transforms x 2.5 w log2 w + 20 L M per codeword-iteration; each transform "
                                 "runs in one workgroup's LDS, so HBM sees only beta, z and the tables",
                         "kernel_ms": {k: round(v[0], 3) for k, v in ph.items()},

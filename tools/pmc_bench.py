@@ -53,16 +53,39 @@ if bp:
                      "algorithmic_bytes_per_codeword_iteration": bp.get("roofline_hbm", bp["roofline"]).get(
                          "algorithmic_bytes_per_codeword_iteration"),
                      "codeword_iterations_per_dispatch": units}
-sc = bench.get("sc")
-if sc:
-    units = sc["batch_per_gpu"] * sc["avg_iterations"]
-    ks = [n for n in per if n.startswith("blk_")]
-    b = sum((per[n]["read_bytes_per_dispatch"] + per[n]["write_bytes_per_dispatch"]) for n in ks)
-    out["sc"] = {"kernels": ks, "hbm_bytes_per_codeword_iteration_approx": b / (units / (sc["avg_iterations"] + 1) * 1.0)
-                 if units else None,
-                 "note": "bytes of one launch of each block-engine kernel divided by the codewords of the batch "
-                         "(one launch = one AMP iteration of the batch)"}
-    if units:
-        out["sc"]["hbm_bytes_per_codeword_iteration_approx"] = b / sc["batch_per_gpu"]
+def windows(path, counter, engine_prefix):
+    """HBM bytes of every dispatch between the first and the last dispatch
+    of an engine's kernels (its decodes, with their control kernels and
+    memsets), and the number of that engine's az dispatches in it."""
+    rows = []
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter:
+            name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("sg::", "")
+            rows.append((int(r["Dispatch_Id"]), name, float(r["Counter_Value"])))
+    ids = [i for i, n, _ in rows if n.startswith((engine_prefix + "ab", engine_prefix + "az"))]
+    if not ids:
+        return 0.0, 0
+    lo, hi = min(ids), max(ids)
+    tot = sum(v for i, _, v in rows if lo <= i <= hi)
+    naz = len({i for i, n, _ in rows if n.startswith(engine_prefix + "az")})
+    return tot, naz
+
+
+for key, prefix in (("sc", "blk_"), ("sc_notebook", "blk2_")):
+    line = bench.get(key)
+    if not line or not line.get("roofline", {}).get("launches"):
+        continue
+    fb, naz = windows(sys.argv[1], "FETCH_SIZE", prefix)
+    wb, _ = windows(sys.argv[2], "WRITE_SIZE", prefix)
+    steps_t = max(1, round(line["roofline"]["launches"].get("az_passB", 0) / max(1, line["avg_iterations"])))
+    az_per_decode = line["roofline"]["launches"].get("az_passB", 0) / max(1, steps_t)
+    decodes = naz / az_per_decode if az_per_decode else 0
+    units = decodes * line["batch_per_gpu"] * line["avg_iterations"]
+    b = 2.0 * fb * 1024 + wb * 1024
+    out[key] = {"engine_kernels": prefix + "*", "decodes_in_window": decodes, "codeword_iterations": units,
+                "hbm_bytes_per_codeword_iteration": b / units if units else None,
+                "note": "FETCH x2 + WRITE of every dispatch from the first to the last block-engine dispatch "
+                        "(decodes incl. control kernels), over the executed codeword-iterations"}
+
 json.dump(out, open(sys.argv[4], "w"), indent=1)
 print(json.dumps(out, indent=1))
