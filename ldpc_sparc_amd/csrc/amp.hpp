@@ -8,6 +8,13 @@ namespace sg {
 
 constexpr int AMP_MAX_EPT = 32;
 
+// Stage twiddles of the block engines' 2^14-point transforms: bit 0 forward,
+// bit 1 inverse from the hardware sine / cosine, otherwise from the plan's
+// table (tb.stw)
+#ifndef SG_BLK_SINCOS
+#define SG_BLK_SINCOS 2
+#endif
+
 // Design operator tables of one design (all transforms), device pointers.
 // A "transform" is one nonzero block (r, c) of the base matrix W
 // (sparc.py:777-875): a sub-sampled DCT of size w with its own orders.

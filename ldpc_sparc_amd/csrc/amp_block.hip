@@ -87,15 +87,20 @@ __device__ __forceinline__ void bk_pos_load(const BlkTables &tb, int t, int tid,
 __device__ __forceinline__ uint32_t bk_pos(const uint32_t *pv, int i) { return (pv[i >> 1] >> (16 * (i & 1))) & 0xffffu; }
 
 // The first three stages of the 2^14-point FFT of fft.hpp (radix 16, 16, 16,
-// then 4; stage twiddles tb.stw as lds_fft1_ct): the forward transform stops
-// before the radix-4 stage, which blk_ab folds into the needed outputs.
+// then 4; stage twiddles from the hardware sine / cosine): the forward
+// transform stops before the radix-4 stage, which blk_ab folds into the
+// needed outputs.
 __device__ __forceinline__ void bk_fwd_stages(cx<float> *d, const cx<float> *__restrict__ stw, int tid) {
-    cx<float> w0[1], w1[6], w2[6];
-    fft1_tw_load_ct<float, 16, BK_LOG2N, 1>(stw, tid, w1);
-    stockham1_stage_ct<float, false, 16, 16, BK_LOG2N, 0>(d, w0, tid);
-    fft1_tw_load_ct<float, 16, BK_LOG2N, 2>(stw, tid, w2);
-    stockham1_stage_ct<float, false, 16, 16, BK_LOG2N, 4>(d, w1, tid);
-    stockham1_stage_ct<float, false, 16, 16, BK_LOG2N, 8>(d, w2, tid);
+    if constexpr (SG_BLK_SINCOS & 1) {
+        lds_fft1_sincos<false, 16, BK_LOG2N, 0, 3>(d, tid);
+    } else {
+        cx<float> w0[1], w1[6], w2[6];
+        fft1_tw_load_ct<float, 16, BK_LOG2N, 1>(stw, tid, w1);
+        stockham1_stage_ct<float, false, 16, 16, BK_LOG2N, 0>(d, w0, tid);
+        fft1_tw_load_ct<float, 16, BK_LOG2N, 2>(stw, tid, w2);
+        stockham1_stage_ct<float, false, 16, 16, BK_LOG2N, 4>(d, w1, tid);
+        stockham1_stage_ct<float, false, 16, 16, BK_LOG2N, 8>(d, w2, tid);
+    }
 }
 
 // ------------------------------------------------------------------ Ab
@@ -216,7 +221,10 @@ __global__ __launch_bounds__(BK_THREADS) void blk_az(BlkTables tb, AmpBufs<float
             if (tl + k * BK_THREADS < ng) d[gl[k]] = gv[k];
         for (int g = tl + 2 * BK_THREADS; g < ng; g += BK_THREADS) d[tb.gloc[g0 + g]] = gcw[g0 + g];
         __syncthreads();
-        if (!(tb.skip & 2)) lds_fft1_ct<float, true, 16, BK_LOG2N>(d, tb.stw, tl);
+        if (!(tb.skip & 2)) {
+            if constexpr (SG_BLK_SINCOS & 2) lds_fft1_sincos<true, 16, BK_LOG2N, 0, 4>(d, tl);
+            else lds_fft1_ct<float, true, 16, BK_LOG2N>(d, tb.stw, tl);
+        }
 #pragma unroll
         for (int i = 0; i < BK_J; ++i)
             u[i] += dr[(pl[(i >> 1) * BK_THREADS + tl] >> (16 * (i & 1))) & 0xffffu];

@@ -83,12 +83,16 @@ __device__ __forceinline__ uint32_t b2_pos(const uint32_t *pv, int i) { return (
 
 // the first three stages (radix 16) of the P-point FFT, as amp_block.hip
 __device__ __forceinline__ void b2_fwd_stages(cx<float> *d, const cx<float> *__restrict__ stw, int tid) {
-    cx<float> w0[1], w1[6], w2[6];
-    fft1_tw_load_ct<float, 16, B2_LOG2P, 1>(stw, tid, w1);
-    stockham1_stage_ct<float, false, 16, 16, B2_LOG2P, 0>(d, w0, tid);
-    fft1_tw_load_ct<float, 16, B2_LOG2P, 2>(stw, tid, w2);
-    stockham1_stage_ct<float, false, 16, 16, B2_LOG2P, 4>(d, w1, tid);
-    stockham1_stage_ct<float, false, 16, 16, B2_LOG2P, 8>(d, w2, tid);
+    if constexpr (SG_BLK_SINCOS & 1) {
+        lds_fft1_sincos<false, 16, B2_LOG2P, 0, 3>(d, tid);
+    } else {
+        cx<float> w0[1], w1[6], w2[6];
+        fft1_tw_load_ct<float, 16, B2_LOG2P, 1>(stw, tid, w1);
+        stockham1_stage_ct<float, false, 16, 16, B2_LOG2P, 0>(d, w0, tid);
+        fft1_tw_load_ct<float, 16, B2_LOG2P, 2>(stw, tid, w2);
+        stockham1_stage_ct<float, false, 16, 16, B2_LOG2P, 4>(d, w1, tid);
+        stockham1_stage_ct<float, false, 16, 16, B2_LOG2P, 8>(d, w2, tid);
+    }
 }
 
 }  // namespace
@@ -179,7 +183,8 @@ __global__ __launch_bounds__(B2_THREADS) void blk2_az(BlkTables tb, AmpBufs<floa
                 atomicAdd(&dst->y, v.y);
             }
             __syncthreads();
-            lds_fft1_ct_lean<float, true, 16, B2_LOG2P>(d, tb.stw, tl);  // no twiddles in flight: u[] stays in registers
+            if constexpr (SG_BLK_SINCOS & 2) lds_fft1_sincos<true, 16, B2_LOG2P, 0, 4>(d, tl);
+            else lds_fft1_ct_lean<float, true, 16, B2_LOG2P>(d, tb.stw, tl);  // no twiddles in flight: u[] stays in registers
             uint32_t pv[B2_J / 2];
             b2_pos_load(tb, t, tl, pv);
 #pragma unroll

@@ -492,6 +492,39 @@ __device__ __forceinline__ void lds_fft1_ct(cx<T> *d, const cx<T> *__restrict__ 
     lds_fft1_ct_from<T, INV, EPT, LOG2N, 0>(d, stw, tid, w0);
 }
 
+// Stage ST of the same plan with its stage twiddles w_(Ns R)^(e k) from the
+// hardware sine / cosine instead of the table (single precision): the
+// argument is in revolutions and (e k mod Ns R) / (Ns R) is exact, and no
+// global load sits between the transform's barriers.
+template <bool INV, int EPT, int LOG2N, int ST>
+__device__ __forceinline__ void fft1_stage_sincos(cx<float> *d, int tid) {
+    constexpr int R = fft1_radix_ct(LOG2N, EPT, ST), LNS = fft1_log2ns_ct(LOG2N, EPT, ST);
+    constexpr int NB = EPT / R, TWN = tw_per_k(R), NTHR = (1 << LOG2N) / EPT;
+    constexpr int LR = R == 2 ? 1 : R == 4 ? 2 : R == 8 ? 3 : 4;
+    cx<float> wl[LNS > 0 ? NB * TWN : 1];
+    if constexpr (LNS > 0) {
+        constexpr float inv = 1.0f / (float)(1 << (LNS + LR));
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            const int k = (tid + i * NTHR) & ((1 << LNS) - 1);
+#pragma unroll
+            for (int q = 0; q < TWN; ++q) {
+                const float x = (float)((tw_exp(R, q) * k) & ((1 << (LNS + LR)) - 1)) * inv;
+                wl[i * TWN + q] = {__builtin_amdgcn_cosf(x), -__builtin_amdgcn_sinf(x)};
+            }
+        }
+    }
+    stockham1_stage_ct<float, INV, R, EPT, LOG2N, LNS>(d, wl, tid);
+}
+// stages ST0 .. ST1 - 1
+template <bool INV, int EPT, int LOG2N, int ST0, int ST1>
+__device__ __forceinline__ void lds_fft1_sincos(cx<float> *d, int tid) {
+    if constexpr (ST0 < ST1) {
+        fft1_stage_sincos<INV, EPT, LOG2N, ST0>(d, tid);
+        lds_fft1_sincos<INV, EPT, LOG2N, ST0 + 1, ST1>(d, tid);
+    }
+}
+
 // Variant without the next stage's twiddles in flight (fewer live registers
 // for kernels that hold other state across the FFT)
 template <typename T, bool INV, int EPT, int LOG2N, int ST>

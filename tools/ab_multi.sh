@@ -2,10 +2,11 @@
 # Same-box A/B of several library builds on the C2 bench line: the current
 # build ("base") and every ldpc_sparc_amd/_lib_v_<name>/ (loaded through
 # LDPC_SPARC_AMD_LIB), interleaved twice.  Output: gpurun_out/abm/<name><i>.json
+# AB_ARGS overrides the bench arguments (default: the C2 line only).
 set -e
 cd "$GRAFT_REPO_ROOT"
 rm -rf gpurun_out/abm; mkdir -p gpurun_out/abm
-A="--no-bp --no-sc --no-sc-notebook --no-concat --no-r13 --cpu-seconds 0"
+A=${AB_ARGS:-"--no-bp --no-sc --no-sc-notebook --no-concat --no-r13 --cpu-seconds 0"}
 for i in 1 2; do
   timeout -k 10 200 python bench.py $A > gpurun_out/abm/base$i.json 2>/dev/null
   for d in ldpc_sparc_amd/_lib_v_*; do
