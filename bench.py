@@ -533,7 +533,7 @@ def sc_bench(args, d, comm, cpu_seconds, procs, L=1024, B=None, steps=None, seed
                         "traffic_unit": "HBM bytes per executed codeword-iteration: every dispatch of the "
                                         f"engine's decodes (PMC, profiles/{sc_tfile})",
                         "kernel": ("blk2_ab + blk_g + blk2_az + control (amp_block2.hip)" if "two-class" in engine else
-                                   "blk_ab + blk_g + blk_az + control (amp_block.hip)") if "block" in engine else
+                                   "blk_az (G slots inline, the next iteration's Ab fused) + control (amp_block.hip)") if "block" in engine else
                                   "general four-step kernels (amp_dct.hip)",
                         "algorithmic_flops_per_codeword_iteration": flops,
                         "algorithmic_bytes_per_codeword_iteration": 4 * (2 * L * M + 4 * n),

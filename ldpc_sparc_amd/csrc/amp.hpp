@@ -228,9 +228,8 @@ template <typename T>
 int amp_launch_cast(const void *in, int in_is_double, T *out, size_t n, hipStream_t s);
 template <typename T>
 int amp_launch_uncast(const T *in, double *out, size_t n, hipStream_t s);
-int blk_launch_ab(const BlkTables &tb, const AmpBufs<float> &bf, hipStream_t s);   // beta -> rbuf
-int blk_launch_az(const BlkTables &tb, const AmpBufs<float> &bf, cx<float> *gbuf,
-                  hipStream_t s);
+int blk_launch_az(const BlkTables &tb, const AmpBufs<float> &bf, bool then_ab,
+                  hipStream_t s);  // z/phi -> G -> beta, section statistics (then the next Ab)
 int blk_launch_g(const BlkTables &tb, const AmpBufs<float> &bf, cx<float> *gbuf, hipStream_t s);  // G slots
 // two-class form for w = 2^16 (amp_block2.hip)
 int blk2_launch_ab(const BlkTables &tb, const AmpBufs<float> &bf, hipStream_t s);

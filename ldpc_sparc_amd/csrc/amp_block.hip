@@ -10,14 +10,17 @@
 // One workgroup owns one column block c of one codeword and runs the omega
 // transforms of that column back to back, each entirely in LDS (Makhoul-packed
 // N2-point FFT, natural order at fsw positions):
-//   blk_ab   beta_c (registers, loaded once) -> for each transform (r, c):
-//            scatter by order1, forward FFT, the Mr needed outputs
-//            Re(c1 H[a] + c2 conj H[b]) -> rbuf[t] (summed per row block in a
-//            fixed order by the control kernel)
+//   Ab       beta_c (registers) -> for each transform (r, c): scatter by
+//            order1, forward FFT, the Mr needed outputs Re(c1 H[a] + c2 conj
+//            H[b]) -> rbuf[t] (summed per row block in a fixed order by the
+//            control kernel); run at the end of the previous iteration's blk_az
 //   blk_az   for each transform (r, c): G from z_r / phi_r (<= 4 terms per
 //            slot), inverse FFT, gather by order1 into u (registers); then the
 //            column's sections: s = beta + tau_c u, softmax, MAP index and the
-//            section statistics of eta_kernel (amp_dct.hip), beta written back.
+//            section statistics of eta_kernel (amp_dct.hip), beta written back;
+//            then (all but the last iteration) the next iteration's Ab
+//            work for the column from the new beta_c in registers, so HBM
+//            reads beta once per iteration.
 // Versus the general four-step path (amp_dct.hip) no transform intermediate
 // reaches HBM and the random-order gather of u happens in LDS.
 #include "amp.hpp"
@@ -88,7 +91,7 @@ __device__ __forceinline__ uint32_t bk_pos(const uint32_t *pv, int i) { return (
 
 // The first three stages of the 2^14-point FFT of fft.hpp (radix 16, 16, 16,
 // then 4; stage twiddles from the hardware sine / cosine): the forward
-// transform stops before the radix-4 stage, which blk_ab folds into the
+// transform stops before the radix-4 stage, which Ab folds into the
 // needed outputs.
 __device__ __forceinline__ void bk_fwd_stages(cx<float> *d, const cx<float> *__restrict__ stw, int tid) {
     if constexpr (SG_BLK_SINCOS & 1) {
@@ -104,18 +107,12 @@ __device__ __forceinline__ void bk_fwd_stages(cx<float> *d, const cx<float> *__r
 }
 
 // ------------------------------------------------------------------ Ab
-template <int EPS>
-__global__ __launch_bounds__(BK_THREADS) void blk_ab(BlkTables tb, AmpBufs<float> bf) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+// The omega forward transforms of column block c from beta_c in registers
+// (bv[i] = beta_c[bk_j(tid, i)])
+__device__ __forceinline__ void bk_ab_column(const BlkTables &tb, const AmpBufs<float> &bf, int c, int cw, int tid,
+                                             const float *bv, unsigned char *smem) {
     cx<float> *d = reinterpret_cast<cx<float> *>(smem);
     float *dr = reinterpret_cast<float *>(smem);
-    const int c = blockIdx.x, cw = blockIdx.y, tid = threadIdx.x;
-    if (!bf.active[cw]) return;
-    const float *beta = bf.beta + (size_t)cw * tb.LM + (size_t)c * tb.Mc;
-    // beta_c once for the column's omega transforms (HBM reads it once)
-    float bv[BK_J];
-#pragma unroll
-    for (int i = 0; i < BK_J; ++i) bv[i] = beta[bk_j<EPS>(tid, i)];
     for (int q = tb.col_ptr[c]; q < tb.col_ptr[c + 1]; ++q) {
         const int t = tb.col_t[q];
         const int tl = bk_opaque(tid);
@@ -156,11 +153,7 @@ __global__ __launch_bounds__(BK_THREADS) void blk_ab(BlkTables tb, AmpBufs<float
 // Makhoul packing): G[k] = sum of <= 4 terms c * z_i / phi_r, one thread per
 // slot, written to gbuf so that blk_az loads each transform's slots in one
 // coalesced round trip.
-__global__ __launch_bounds__(256) void blk_g(BlkTables tb, AmpBufs<float> bf, cx<float> *gbuf) {
-    const int cw = blockIdx.y;
-    if (!bf.active[cw]) return;
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= tb.ngs) return;
+__device__ __forceinline__ cx<float> bk_gslot(const BlkTables &tb, const AmpBufs<float> &bf, int cw, int g) {
     const int row = tb.grow[g];
     const float *z = bf.z + (size_t)cw * tb.n + (size_t)row * tb.Mr;
     const float phi = (float)bf.phi[(size_t)cw * tb.Lr + row];
@@ -175,12 +168,21 @@ __global__ __launch_bounds__(256) void blk_g(BlkTables tb, AmpBufs<float> bf, cx
             acc.y += cc.y * v;
         }
     }
-    gbuf[(size_t)cw * tb.ngs + g] = acc;
+    return acc;
+}
+__global__ __launch_bounds__(256) void blk_g(BlkTables tb, AmpBufs<float> bf, cx<float> *gbuf) {
+    const int cw = blockIdx.y;
+    if (!bf.active[cw]) return;
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= tb.ngs) return;
+    gbuf[(size_t)cw * tb.ngs + g] = bk_gslot(tb, bf, cw, g);
 }
 
 // ------------------------------------------------------------------ Az + eta
+// with do_ab: then the next iteration's forward transforms of the column from
+// the new beta_c still in registers (bk_ab_column; beta_c is not read back)
 template <int EPS>
-__global__ __launch_bounds__(BK_THREADS) void blk_az(BlkTables tb, AmpBufs<float> bf, const cx<float> *gbuf) {
+__global__ __launch_bounds__(BK_THREADS) void blk_az(BlkTables tb, AmpBufs<float> bf, int do_ab) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     cx<float> *d = reinterpret_cast<cx<float> *>(smem);
     float *dr = reinterpret_cast<float *>(smem);
@@ -192,13 +194,12 @@ __global__ __launch_bounds__(BK_THREADS) void blk_az(BlkTables tb, AmpBufs<float
     float u[BK_J];
 #pragma unroll
     for (int i = 0; i < BK_J; ++i) u[i] = 0.f;
-    const cx<float> *gcw = gbuf + (size_t)cw * tb.ngs;
     // Az(z / phi) restricted to column block c, summed over its transforms in
     // the order of gather_u (amp_dct.hip)
     for (int q = tb.col_ptr[c]; q < tb.col_ptr[c + 1]; ++q) {
         const int t = tb.col_t[q];
         const int tl = bk_opaque(tid);
-        // one round trip: positions and G slots, in flight while the image clears
+        // positions and G slots (from z / phi, <= 4 terms), in flight while the image clears
         uint32_t pv[BK_J / 2];
         bk_pos_load(tb, t, tl, pv);
         const int g0 = tb.gptr[t], ng = tb.gptr[t + 1] - g0;
@@ -208,7 +209,7 @@ __global__ __launch_bounds__(BK_THREADS) void blk_az(BlkTables tb, AmpBufs<float
         for (int k = 0; k < 2; ++k) {
             const int g = tl + k * BK_THREADS;
             if (g < ng) {
-                gv[k] = gcw[g0 + g];
+                gv[k] = bk_gslot(tb, bf, cw, g0 + g);
                 gl[k] = tb.gloc[g0 + g];
             }
         }
@@ -219,7 +220,7 @@ __global__ __launch_bounds__(BK_THREADS) void blk_az(BlkTables tb, AmpBufs<float
 #pragma unroll
         for (int k = 0; k < 2; ++k)
             if (tl + k * BK_THREADS < ng) d[gl[k]] = gv[k];
-        for (int g = tl + 2 * BK_THREADS; g < ng; g += BK_THREADS) d[tb.gloc[g0 + g]] = gcw[g0 + g];
+        for (int g = tl + 2 * BK_THREADS; g < ng; g += BK_THREADS) d[tb.gloc[g0 + g]] = bk_gslot(tb, bf, cw, g0 + g);
         __syncthreads();
         if (!(tb.skip & 2)) {
             if constexpr (SG_BLK_SINCOS & 2) lds_fft1_sincos<true, 16, BK_LOG2N, 0, 4>(d, tl);
@@ -241,7 +242,7 @@ __global__ __launch_bounds__(BK_THREADS) void blk_az(BlkTables tb, AmpBufs<float
     const int nsec = tb.Mc / tb.M;
     const float tau = (float)bf.tau[(size_t)cw * tb.Lc + c];
     float *beta = bf.beta + (size_t)cw * tb.LM + (size_t)c * tb.Mc;
-    float s[BK_J], x[BK_J];
+    float s[BK_J], x[BK_J], bv[BK_J];
 #pragma unroll
     for (int i = 0; i < BK_J; ++i) {
         const int j = bk_j<EPS>(tid, i);
@@ -280,6 +281,7 @@ __global__ __launch_bounds__(BK_THREADS) void blk_az(BlkTables tb, AmpBufs<float
         for (int e = 0; e < eps; ++e) {
             const float b = x[i0 + e] / dn;
             beta[ls * tb.M + lane * eps + e] = b;
+            bv[i0 + e] = b;
             const float dl = b - ((lane * eps + e) == truth ? 1.f : 0.f);
             ss += b * b;
             se += dl * dl;
@@ -293,13 +295,16 @@ __global__ __launch_bounds__(BK_THREADS) void blk_az(BlkTables tb, AmpBufs<float
             bf.sec_argmax[o] = arg;
         }
     }
+    if (do_ab) {
+        __syncthreads();
+        bk_ab_column(tb, bf, c, cw, tid, bv, smem);
+    }
 }
 
 template <int EPS>
 static int blk_set_attrs(size_t lds) {
     static size_t done = 0;
     if (done >= lds) return SG_OK;
-    SG_HIP(hipFuncSetAttribute((const void *)blk_ab<EPS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     SG_HIP(hipFuncSetAttribute((const void *)blk_az<EPS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     done = lds;
     return SG_OK;
@@ -318,26 +323,10 @@ static int blk_set_attrs(size_t lds) {
     }
 
 template <int EPS>
-static void bk_launch_ab(const BlkTables &tb, const AmpBufs<float> &bf, size_t lds, hipStream_t s, int *rc) {
+static void bk_launch_az(const BlkTables &tb, const AmpBufs<float> &bf, int do_ab, size_t lds, hipStream_t s,
+                         int *rc) {
     *rc = blk_set_attrs<EPS>(lds);
-    if (*rc == SG_OK) hipLaunchKernelGGL(blk_ab<EPS>, dim3(tb.Lc, bf.B), dim3(BK_THREADS), lds, s, tb, bf);
-}
-template <int EPS>
-static void bk_launch_az(const BlkTables &tb, const AmpBufs<float> &bf, const cx<float> *gbuf, size_t lds,
-                         hipStream_t s, int *rc) {
-    *rc = blk_set_attrs<EPS>(lds);
-    if (*rc == SG_OK) hipLaunchKernelGGL(blk_az<EPS>, dim3(tb.Lc, bf.B), dim3(BK_THREADS), lds, s, tb, bf, gbuf);
-}
-
-int blk_launch_ab(const BlkTables &tb, const AmpBufs<float> &bf, hipStream_t s) {
-    if (bf.B <= 0) return SG_OK;
-    const size_t lds = blk_lds_bytes(tb.Mc);
-    int rc = SG_OK;
-    ProfScope ps(SG_PH_AB_A, s);
-    BK_EPS_DISPATCH(tb.M, bk_launch_ab, tb, bf, lds, s, &rc);
-    SG_TRY(rc);
-    SG_HIP(hipGetLastError());
-    return SG_OK;
+    if (*rc == SG_OK) hipLaunchKernelGGL(blk_az<EPS>, dim3(tb.Lc, bf.B), dim3(BK_THREADS), lds, s, tb, bf, do_ab);
 }
 
 int blk_launch_g(const BlkTables &tb, const AmpBufs<float> &bf, cx<float> *gbuf, hipStream_t s) {
@@ -348,13 +337,12 @@ int blk_launch_g(const BlkTables &tb, const AmpBufs<float> &bf, cx<float> *gbuf,
     return SG_OK;
 }
 
-int blk_launch_az(const BlkTables &tb, const AmpBufs<float> &bf, cx<float> *gbuf, hipStream_t s) {
+int blk_launch_az(const BlkTables &tb, const AmpBufs<float> &bf, bool then_ab, hipStream_t s) {
     if (bf.B <= 0) return SG_OK;
     const size_t lds = blk_lds_bytes(tb.Mc);
-    SG_TRY(blk_launch_g(tb, bf, gbuf, s));
     int rc = SG_OK;
     ProfScope ps(SG_PH_AZ_B, s);
-    BK_EPS_DISPATCH(tb.M, bk_launch_az, tb, bf, (const cx<float> *)gbuf, lds, s, &rc);
+    BK_EPS_DISPATCH(tb.M, bk_launch_az, tb, bf, then_ab ? 1 : 0, lds, s, &rc);
     SG_TRY(rc);
     SG_HIP(hipGetLastError());
     return SG_OK;
