@@ -209,7 +209,6 @@ __global__ __launch_bounds__(BP_THREADS, (bp_waves_per_simd<T, KIND>())) void bp
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr bool LEAN = bp_lean<T, MAXDC>();
     constexpr bool SCR = LEAN && KIND == SG_SUMPROD2;
-    constexpr bool LEANV = LEAN || VJ > 4;  // variable pass without per-port register arrays
     T *msg = reinterpret_cast<T *>(smem);
     T *scr = msg + (SCR ? a.slots : 0);                         // Lxfb backward values (lean sumprod2)
     uint16_t *ps = reinterpret_cast<uint16_t *>(msg + (SCR ? 2 : 1) * a.slots);  // variable port -> message slot
@@ -232,7 +231,10 @@ __global__ __launch_bounds__(BP_THREADS, (bp_waves_per_simd<T, KIND>())) void bp
         __syncthreads();
         int it = 0;
         for (; it < a.max_it; ++it) {
-            // ---- variable pass (c_ldpc.c:171-178)
+            // ---- variable pass (c_ldpc.c:171-178): two loops over the ports, the
+            // second re-reading the slots (holding them in per-port register
+            // arrays unrolled to the maximum degree measured 5 % slower: divergent
+            // branches and their exec-mask bookkeeping)
 #pragma unroll
             for (int j = 0; j < VJ; ++j) {
                 const int v = tid + j * BP_THREADS;
@@ -240,26 +242,10 @@ __global__ __launch_bounds__(BP_THREADS, (bp_waves_per_simd<T, KIND>())) void bp
                 const int p0 = vo[v];
                 const int d = vo[v + 1] - p0;
                 T acc = chv[j];
-                if constexpr (LEANV) {  // second pass re-reads the slots instead of holding them
-                    for (int k = 0; k < d; ++k) acc += msg[ps[p0 + k]];
-                    for (int k = 0; k < d; ++k) {
-                        const int sl = ps[p0 + k];
-                        msg[sl] = acc - msg[sl];
-                    }
-                } else {
-                    int s[BP_MAXDV];
-                    T m[BP_MAXDV];
-#pragma unroll
-                    for (int k = 0; k < BP_MAXDV; ++k)
-                        if (k < d) { s[k] = ps[p0 + k]; m[k] = msg[s[k]]; acc += m[k]; }
-                    for (int k = BP_MAXDV; k < d; ++k) acc += msg[ps[p0 + k]];
-#pragma unroll
-                    for (int k = 0; k < BP_MAXDV; ++k)
-                        if (k < d) msg[s[k]] = acc - m[k];
-                    for (int k = BP_MAXDV; k < d; ++k) {
-                        const int sl = ps[p0 + k];
-                        msg[sl] = acc - msg[sl];
-                    }
+                for (int k = 0; k < d; ++k) acc += msg[ps[p0 + k]];
+                for (int k = 0; k < d; ++k) {
+                    const int sl = ps[p0 + k];
+                    msg[sl] = acc - msg[sl];
                 }
                 apv[j] = acc;
             }

@@ -5,7 +5,6 @@
 namespace sg {
 
 constexpr int BP_THREADS = 512;
-constexpr int BP_MAXDV = 12;            // variable degrees above this take a slower loop
 constexpr int BP_VJ = 8;                // variables per thread held in registers (nv <= BP_VJ * BP_THREADS)
 constexpr int BP_MAX_LDS = 160 * 1024;  // one workgroup's LDS limit on gfx950
 
