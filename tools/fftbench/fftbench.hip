@@ -391,6 +391,44 @@ static std::vector<float2> check(void) {
     return h;
 }
 
+// occupancy study: NT threads run nf transforms of 2^LOG2N points (EPT 8,
+// sine/cosine stage twiddles, fft.hpp lds_fft1_sincos); LDS requested per
+// workgroup sets how many workgroups share a CU
+template <int LOG2N, int NT>
+__global__ __launch_bounds__(NT) void occ_bench(float *out, long long *cyc, int nf) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cx<float> *A = reinterpret_cast<cx<float> *>(smem);
+    const int tid = threadIdx.x;
+    for (int i = tid; i < (1 << LOG2N); i += NT) A[i] = {(float)(i & 7), (float)(blockIdx.x & 3)};
+    __syncthreads();
+    const long long t0 = clock64();
+    for (int f = 0; f < nf; ++f) lds_fft1_sincos<false, 8, LOG2N, 0, fft1_nstages_ct(LOG2N, 8)>(A, opaque(tid));
+    const long long t1 = clock64();
+    if (tid == 0) cyc[blockIdx.x] = t1 - t0;
+    out[blockIdx.x * NT + tid] = A[tid].x;
+}
+template <int LOG2N, int NT>
+static void occ_run(const char *name, int nb, int nf, int lds) {
+    float *out;
+    long long *cyc;
+    hipMalloc(&out, sizeof(float) * nb * NT);
+    hipMalloc(&cyc, sizeof(long long) * nb);
+    hipFuncSetAttribute((const void *)occ_bench<LOG2N, NT>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL((occ_bench<LOG2N, NT>), dim3(nb), dim3(NT), lds, 0, out, cyc, nf);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipEventRecord(e0);
+    hipLaunchKernelGGL((occ_bench<LOG2N, NT>), dim3(nb), dim3(NT), lds, 0, out, cyc, nf);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    printf("%s: %.1f us wall for %d workgroups x %d transforms of 2^%d\n", name, ms * 1e3, nb, nf, LOG2N);
+    hipFree(out);
+    hipFree(cyc);
+}
+
 template <bool INV>
 __global__ __launch_bounds__(T) void check_wfft(float2 *out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -471,6 +509,11 @@ int main() {
     run<6>(nb, nf);
     run<7>(nb, nf);
     run<8>(nb, nf);
+    // one codeword-iteration's forward transforms per CU: 64 x 2^13 in one
+    // workgroup against 128 x 2^12 in two workgroups sharing the CU
+    occ_run<13, 1024>("occupancy: 1 workgroup/CU, 1024 threads, 64 x 8192", 256, 64, 160 * 1024);
+    occ_run<12, 512>("occupancy: 2 workgroups/CU, 512 threads, 64 x 4096 each", 512, 64, 80 * 1024);
+    occ_run<12, 512>("occupancy: 1 workgroup/CU, 512 threads, 128 x 4096", 256, 128, 160 * 1024);
     grun<1024, 8, 0, false>("g1024x8 r8 2bar", nb, nf);
     grun<512, 16, 0, false>("g512x16 r8 2bar", nb, nf);
     grun<512, 16, 0, true>("g512x16 r8 pingpong", nb, nf);
