@@ -28,6 +28,13 @@
 
 namespace sg {
 
+// ports per round of the variable pass, and the padding of the LDS port
+// table that lets a round read past the last variable's ports
+#ifndef BP_VU
+#define BP_VU 2
+#endif
+constexpr int BP_PS_PAD = BP_VU;
+
 template <typename T>
 __device__ __forceinline__ T dev_log(T x);
 template <>
@@ -193,7 +200,7 @@ constexpr bool bp_lean() { return sizeof(T) == 8 || MAXDC > 8; }
 template <typename T>
 size_t bp_lds_bytes(int slots, int nv, int nports, int nc, bool scratch = false) {
     size_t b = sizeof(T) * (size_t)slots * (scratch ? 2 : 1);
-    b += sizeof(uint16_t) * ((size_t)nports + nv + 1) + nc;
+    b += sizeof(uint16_t) * ((size_t)nports + BP_PS_PAD + nv + 1) + nc;
     return (b + 15) / 16 * 16;
 }
 
@@ -212,10 +219,10 @@ __global__ __launch_bounds__(BP_THREADS, (bp_waves_per_simd<T, KIND>())) void bp
     T *msg = reinterpret_cast<T *>(smem);
     T *scr = msg + (SCR ? a.slots : 0);                         // Lxfb backward values (lean sumprod2)
     uint16_t *ps = reinterpret_cast<uint16_t *>(msg + (SCR ? 2 : 1) * a.slots);  // variable port -> message slot
-    uint16_t *vo = ps + a.nports;                                // variable-port offsets
+    uint16_t *vo = ps + a.nports + BP_PS_PAD;                    // variable-port offsets
     uint8_t *cd = reinterpret_cast<uint8_t *>(vo + a.nv + 1);    // check degrees
     const int tid = threadIdx.x;
-    for (int i = tid; i < a.nports; i += BP_THREADS) ps[i] = (uint16_t)a.port_slot[i];
+    for (int i = tid; i < a.nports + BP_PS_PAD; i += BP_THREADS) ps[i] = i < a.nports ? (uint16_t)a.port_slot[i] : 0;
     for (int i = tid; i <= a.nv; i += BP_THREADS) vo[i] = (uint16_t)a.voff[i];
     for (int i = tid; i < a.nc; i += BP_THREADS) cd[i] = a.cdeg[i];
     for (int cw = blockIdx.x; cw < a.B; cw += gridDim.x) {
@@ -242,10 +249,38 @@ __global__ __launch_bounds__(BP_THREADS, (bp_waves_per_simd<T, KIND>())) void bp
                 const int p0 = vo[v];
                 const int d = vo[v + 1] - p0;
                 T acc = chv[j];
-                for (int k = 0; k < d; ++k) acc += msg[ps[p0 + k]];
-                for (int k = 0; k < d; ++k) {
-                    const int sl = ps[p0 + k];
-                    msg[sl] = acc - msg[sl];
+                if constexpr (BP_VU > 1) {
+                    // BP_VU ports per round: their table and message reads issued
+                    // together (one LDS round trip per round instead of per port);
+                    // ports past d read a padded table entry and are not used, and
+                    // acc takes the ports in order (c_ldpc.c:171-178)
+                    for (int k = 0; k < d; k += BP_VU) {
+                        int sl[BP_VU];
+                        T m[BP_VU];
+#pragma unroll
+                        for (int u = 0; u < BP_VU; ++u) sl[u] = ps[p0 + k + u];
+#pragma unroll
+                        for (int u = 0; u < BP_VU; ++u) m[u] = msg[sl[u]];
+#pragma unroll
+                        for (int u = 0; u < BP_VU; ++u) acc = k + u < d ? acc + m[u] : acc;
+                    }
+                    for (int k = 0; k < d; k += BP_VU) {
+                        int sl[BP_VU];
+                        T m[BP_VU];
+#pragma unroll
+                        for (int u = 0; u < BP_VU; ++u) sl[u] = ps[p0 + k + u];
+#pragma unroll
+                        for (int u = 0; u < BP_VU; ++u) m[u] = msg[sl[u]];
+#pragma unroll
+                        for (int u = 0; u < BP_VU; ++u)
+                            if (k + u < d) msg[sl[u]] = acc - m[u];
+                    }
+                } else {
+                    for (int k = 0; k < d; ++k) acc += msg[ps[p0 + k]];
+                    for (int k = 0; k < d; ++k) {
+                        const int sl = ps[p0 + k];
+                        msg[sl] = acc - msg[sl];
+                    }
                 }
                 apv[j] = acc;
             }
