@@ -62,20 +62,65 @@ __device__ __forceinline__ cx<float> cw_w(const CwTables &tb, uint32_t j) {
 }
 
 // Radix plan of the P-point FFT at 8 values per thread (CW_RADIX_PLAN 0:
-// fft.hpp's 4, 4, 8, 8, 8; 1: 8, 8, 8, 8, 2; 2: 2, 8, 8, 8, 8)
+// fft.hpp's 4, 4, 8, 8, 8; 1: 8, 8, 8, 8, 2; 2: 2, 8, 8, 8, 8; 3: 16, 8, 8, 8
+// with the radix-16 first stage split over lanes l and l ^ 32, cw_stage0_r16)
 #ifndef CW_RADIX_PLAN
-#define CW_RADIX_PLAN 1
+#define CW_RADIX_PLAN 3
 #endif
-constexpr int cw_nstages() { return 5; }
+constexpr int cw_nstages() { return CW_RADIX_PLAN == 3 ? 4 : 5; }
 constexpr int cw_radix(int st) {
-    return CW_RADIX_PLAN == 0 ? fft1_radix_ct(CW_LOG2P, CW_EPT, st)
+    return CW_RADIX_PLAN == 0   ? fft1_radix_ct(CW_LOG2P, CW_EPT, st)
            : CW_RADIX_PLAN == 1 ? (st < 4 ? 8 : 2)
-                                : (st == 0 ? 2 : 8);
+           : CW_RADIX_PLAN == 2 ? (st == 0 ? 2 : 8)
+                                : (st == 0 ? 16 : 8);
 }
 constexpr int cw_log2ns(int st) {
     int l = 0;
-    for (int i = 0; i < st; ++i) l += cw_radix(i) == 2 ? 1 : cw_radix(i) == 4 ? 2 : 3;
+    for (int i = 0; i < st; ++i) l += cw_radix(i) == 2 ? 1 : cw_radix(i) == 4 ? 2 : cw_radix(i) == 8 ? 3 : 4;
     return l;
+}
+
+// lanes 32..63 of a <-> lanes 0..31 of b (v_permlane32_swap, no LDS)
+__device__ __forceinline__ void cw_swap32(cx<float> &a, cx<float> &b) {
+    const auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.x), __float_as_uint(b.x), false, false);
+    const auto ry = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.y), __float_as_uint(b.y), false, false);
+    a = {__uint_as_float(rx[0]), __uint_as_float(ry[0])};
+    b = {__uint_as_float(rx[1]), __uint_as_float(ry[1])};
+}
+
+// First Stockham stage at radix 16 (Ns = 1, no twiddles) with 8 values per
+// thread: butterfly j = 32 w + (l & 31) of wavefront w is shared by lanes l
+// and l ^ 32, lane half H holding inputs m = 8 H + jj (x[j + 512 m]).  A
+// radix-2 step across the halves (two rounds of permlane32 swaps) and a
+// radix-8 DFT in registers give lane half H the outputs 2 q + H, stored at
+// j 16 + 2 q + H like stockham1_stage_ct's.
+template <bool INV>
+__device__ __forceinline__ void cw_stage0_r16(cx<float> *d, int tid) {
+    const int l = tid & 63, H = l >> 5, j = ((tid >> 6) << 5) | (l & 31);
+    cx<float> v[8];
+    const int jp = fsw(j);  // adding multiples of 256 commutes with the swizzle
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) v[jj] = d[jp + ((8 * H + jj) << 9)];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) cw_swap32(v[jj], v[jj + 4]);  // lane half H: x[J], x[8 + J], J = jj + 4 H
+    {
+        constexpr float c1 = 0.92387953251128675613f, s1 = 0.38268343236508977173f, r2 = 0.70710678118654752440f;
+        const cx<float> w16[4] = {{1.f, 0.f}, {c1, INV ? s1 : -s1}, {r2, INV ? r2 : -r2}, {s1, INV ? c1 : -c1}};
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const cx<float> u = v[jj], x8 = v[jj + 4];
+            v[jj] = cadd(u, x8);
+            const cx<float> t = jj == 0 ? csub(u, x8) : cmul(csub(u, x8), w16[jj]);  // (u - x8) w16^jj
+            v[jj + 4] = H ? mul_mi<float, INV>(t) : t;                                 // * w16^(4 H)
+        }
+    }
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) cw_swap32(v[jj], v[jj + 4]);  // lane half p: y_p[0..7]
+    dft8<float, INV>(v);                                         // v[q] = X_j[2 q + H]
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 8; ++q) d[fsw((j << 4) | (q << 1) | H)] = v[q];
+    __syncthreads();
 }
 
 // The P-point LDS FFT (fft.hpp stages) with its stage twiddles
@@ -83,7 +128,10 @@ constexpr int cw_log2ns(int st) {
 // global loads between its barriers.
 template <bool INV, int ST>
 __device__ __forceinline__ void cw_fft_from(cx<float> *d, int tid) {
-    if constexpr (ST < cw_nstages()) {
+    if constexpr (ST == 0 && cw_radix(0) == 16) {
+        cw_stage0_r16<INV>(d, tid);
+        cw_fft_from<INV, 1>(d, tid);
+    } else if constexpr (ST < cw_nstages()) {
         constexpr int R = cw_radix(ST), LNS = cw_log2ns(ST);
         constexpr int NB = CW_EPT / R, TWN = tw_per_k(R);
         cx<float> wl[LNS > 0 ? NB * TWN : 1];
