@@ -194,13 +194,14 @@ template <typename T, int MAXDC>
 constexpr bool bp_lean() { return sizeof(T) == 8 || MAXDC > 8; }
 
 // LDS image of one workgroup: the messages of its current codeword and --
-// loaded once per workgroup -- the graph tables as 16-bit indices, so the
-// per-iteration passes never leave LDS.  The channel LLRs and the app of the
-// thread's variables (v = tid + BP_THREADS j) stay in registers.
+// loaded once per workgroup -- the port -> slot table (16-bit) and the check
+// degrees, so the per-iteration passes never leave LDS.  The channel LLRs,
+// the app and the port range of the thread's variables (v = tid +
+// BP_THREADS j) stay in registers.
 template <typename T>
 size_t bp_lds_bytes(int slots, int nv, int nports, int nc, bool scratch = false) {
     size_t b = sizeof(T) * (size_t)slots * (scratch ? 2 : 1);
-    b += sizeof(uint16_t) * ((size_t)nports + BP_PS_PAD + nv + 1) + nc;
+    b += sizeof(uint16_t) * ((size_t)nports + BP_PS_PAD) + nc;
     return (b + 15) / 16 * 16;
 }
 
@@ -219,12 +220,19 @@ __global__ __launch_bounds__(BP_THREADS, (bp_waves_per_simd<T, KIND>())) void bp
     T *msg = reinterpret_cast<T *>(smem);
     T *scr = msg + (SCR ? a.slots : 0);                         // Lxfb backward values (lean sumprod2)
     uint16_t *ps = reinterpret_cast<uint16_t *>(msg + (SCR ? 2 : 1) * a.slots);  // variable port -> message slot
-    uint16_t *vo = ps + a.nports + BP_PS_PAD;                    // variable-port offsets
-    uint8_t *cd = reinterpret_cast<uint8_t *>(vo + a.nv + 1);    // check degrees
+    uint8_t *cd = reinterpret_cast<uint8_t *>(ps + a.nports + BP_PS_PAD);  // check degrees
     const int tid = threadIdx.x;
     for (int i = tid; i < a.nports + BP_PS_PAD; i += BP_THREADS) ps[i] = i < a.nports ? (uint16_t)a.port_slot[i] : 0;
-    for (int i = tid; i <= a.nv; i += BP_THREADS) vo[i] = (uint16_t)a.voff[i];
     for (int i = tid; i < a.nc; i += BP_THREADS) cd[i] = a.cdeg[i];
+    // the port range of the thread's variables, constant over iterations and
+    // codewords: held in registers (no offset-table round trip per iteration)
+    int vp0[VJ], vd[VJ];
+#pragma unroll
+    for (int j = 0; j < VJ; ++j) {
+        const int v = tid + j * BP_THREADS;
+        vp0[j] = v < a.nv ? (int)a.voff[v] : 0;
+        vd[j] = v < a.nv ? (int)a.voff[v + 1] - vp0[j] : 0;
+    }
     for (int cw = blockIdx.x; cw < a.B; cw += gridDim.x) {
         const T *ch = a.ch + (size_t)cw * a.nv;
         T chv[VJ], apv[VJ];
@@ -246,8 +254,7 @@ __global__ __launch_bounds__(BP_THREADS, (bp_waves_per_simd<T, KIND>())) void bp
             for (int j = 0; j < VJ; ++j) {
                 const int v = tid + j * BP_THREADS;
                 if (v >= a.nv) continue;
-                const int p0 = vo[v];
-                const int d = vo[v + 1] - p0;
+                const int p0 = vp0[j], d = vd[j];
                 T acc = chv[j];
                 if constexpr (BP_VU > 1) {
                     // BP_VU ports per round: their table and message reads issued
