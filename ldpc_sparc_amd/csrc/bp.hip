@@ -33,7 +33,7 @@ namespace sg {
 #ifndef BP_VU
 #define BP_VU 2
 #endif
-constexpr int BP_PS_PAD = BP_VU;
+constexpr int BP_PS_PAD = 2;
 
 template <typename T>
 __device__ __forceinline__ T dev_log(T x);
@@ -227,11 +227,18 @@ __global__ __launch_bounds__(BP_THREADS, (bp_waves_per_simd<T, KIND>())) void bp
     // the port range of the thread's variables, constant over iterations and
     // codewords: held in registers (no offset-table round trip per iteration)
     int vp0[VJ], vd[VJ];
+    uint32_t vs01[VJ];  // message slots of the first two ports, packed
 #pragma unroll
     for (int j = 0; j < VJ; ++j) {
         const int v = tid + j * BP_THREADS;
         vp0[j] = v < a.nv ? (int)a.voff[v] : 0;
         vd[j] = v < a.nv ? (int)a.voff[v + 1] - vp0[j] : 0;
+        vs01[j] = 0u;
+        if constexpr (!LEAN) {
+            const uint32_t s0 = vd[j] > 0 ? (uint32_t)a.port_slot[vp0[j]] : 0u;
+            const uint32_t s1 = vd[j] > 1 ? (uint32_t)a.port_slot[vp0[j] + 1] : 0u;
+            vs01[j] = s0 | (s1 << 16);
+        }
     }
     for (int cw = blockIdx.x; cw < a.B; cw += gridDim.x) {
         const T *ch = a.ch + (size_t)cw * a.nv;
@@ -256,31 +263,37 @@ __global__ __launch_bounds__(BP_THREADS, (bp_waves_per_simd<T, KIND>())) void bp
                 if (v >= a.nv) continue;
                 const int p0 = vp0[j], d = vd[j];
                 T acc = chv[j];
-                if constexpr (BP_VU > 1) {
-                    // BP_VU ports per round: their table and message reads issued
+                if constexpr (BP_VU == 2) {
+                    // two ports per round: their table and message reads issued
                     // together (one LDS round trip per round instead of per port);
-                    // ports past d read a padded table entry and are not used, and
-                    // acc takes the ports in order (c_ldpc.c:171-178)
-                    for (int k = 0; k < d; k += BP_VU) {
-                        int sl[BP_VU];
-                        T m[BP_VU];
-#pragma unroll
-                        for (int u = 0; u < BP_VU; ++u) sl[u] = ps[p0 + k + u];
-#pragma unroll
-                        for (int u = 0; u < BP_VU; ++u) m[u] = msg[sl[u]];
-#pragma unroll
-                        for (int u = 0; u < BP_VU; ++u) acc = k + u < d ? acc + m[u] : acc;
+                    // a round may read one padded table entry past d, which is not
+                    // used; acc takes the ports in order (c_ldpc.c:171-178).  The
+                    // check-degree <= 8 kernels take the first round's slots from
+                    // registers (vs01): C3 +10 %, but the high-degree (lean)
+                    // kernels measured slower with it
+                    constexpr bool R0 = !LEAN;
+                    const int s0 = (int)(vs01[j] & 0xffffu), s1 = (int)(vs01[j] >> 16);
+                    if constexpr (R0) {
+                        const T m0 = msg[s0], m1 = msg[s1];
+                        acc = d > 0 ? acc + m0 : acc;
+                        acc = d > 1 ? acc + m1 : acc;
                     }
-                    for (int k = 0; k < d; k += BP_VU) {
-                        int sl[BP_VU];
-                        T m[BP_VU];
-#pragma unroll
-                        for (int u = 0; u < BP_VU; ++u) sl[u] = ps[p0 + k + u];
-#pragma unroll
-                        for (int u = 0; u < BP_VU; ++u) m[u] = msg[sl[u]];
-#pragma unroll
-                        for (int u = 0; u < BP_VU; ++u)
-                            if (k + u < d) msg[sl[u]] = acc - m[u];
+                    for (int k = R0 ? 2 : 0; k < d; k += 2) {
+                        const int sa = ps[p0 + k], sb = ps[p0 + k + 1];
+                        const T ma = msg[sa], mb = msg[sb];
+                        acc += ma;
+                        acc = k + 1 < d ? acc + mb : acc;
+                    }
+                    if constexpr (R0) {
+                        const T m0 = msg[s0], m1 = msg[s1];
+                        if (d > 0) msg[s0] = acc - m0;
+                        if (d > 1) msg[s1] = acc - m1;
+                    }
+                    for (int k = R0 ? 2 : 0; k < d; k += 2) {
+                        const int sa = ps[p0 + k], sb = ps[p0 + k + 1];
+                        const T ma = msg[sa], mb = msg[sb];
+                        msg[sa] = acc - ma;
+                        if (k + 1 < d) msg[sb] = acc - mb;
                     }
                 } else {
                     for (int k = 0; k < d; ++k) acc += msg[ps[p0 + k]];
