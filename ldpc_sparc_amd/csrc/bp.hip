@@ -273,8 +273,10 @@ __global__ __launch_bounds__(BP_THREADS, (bp_waves_per_simd<T, KIND>())) void bp
                     // kernels measured slower with it
                     constexpr bool R0 = !LEAN;
                     const int s0 = (int)(vs01[j] & 0xffffu), s1 = (int)(vs01[j] >> 16);
+                    T m0 = T(0), m1 = T(0);  // (only this thread touches its ports' slots in this pass)
                     if constexpr (R0) {
-                        const T m0 = msg[s0], m1 = msg[s1];
+                        m0 = msg[s0];
+                        m1 = msg[s1];
                         acc = d > 0 ? acc + m0 : acc;
                         acc = d > 1 ? acc + m1 : acc;
                     }
@@ -285,7 +287,6 @@ __global__ __launch_bounds__(BP_THREADS, (bp_waves_per_simd<T, KIND>())) void bp
                         acc = k + 1 < d ? acc + mb : acc;
                     }
                     if constexpr (R0) {
-                        const T m0 = msg[s0], m1 = msg[s1];
                         if (d > 0) msg[s0] = acc - m0;
                         if (d > 1) msg[s1] = acc - m1;
                     }
