@@ -60,12 +60,16 @@ __device__ __forceinline__ T lxor(T a, T b) {
     return out;
 }
 
-template <typename T, int KIND, int MAXDC>
-__device__ __forceinline__ bool check_update(T *__restrict__ msg, int c, int nc, int d, T factor) {
-    T L[MAXDC];
+template <typename T, int MAXDC>
+__device__ __forceinline__ void check_load(const T *__restrict__ msg, int c, int nc, int d, T *L) {
 #pragma unroll
     for (int k = 0; k < MAXDC; ++k)
         if (k < d) L[k] = msg[k * nc + c];
+}
+
+// check node update from the check's incoming messages L (check_load)
+template <typename T, int KIND, int MAXDC>
+__device__ __forceinline__ bool check_update_from(T *__restrict__ msg, int c, int nc, int d, T factor, T *L) {
     bool unsat = false;
     if (KIND == SG_MINSUM) {
         // Compressed form of Lxfb(.., corr=0): |out_k| = min over the others,
@@ -128,6 +132,13 @@ __device__ __forceinline__ bool check_update(T *__restrict__ msg, int c, int nc,
             if (k < d) msg[k * nc + c] = T(2) * atanh(prod / L[k]);
     }
     return unsat;
+}
+
+template <typename T, int KIND, int MAXDC>
+__device__ __forceinline__ bool check_update(T *__restrict__ msg, int c, int nc, int d, T factor) {
+    T L[MAXDC];
+    check_load<T, MAXDC>(msg, c, nc, d, L);
+    return check_update_from<T, KIND, MAXDC>(msg, c, nc, d, factor, L);
 }
 
 // Register-lean check update for high check degrees and double precision:
@@ -226,17 +237,19 @@ __global__ __launch_bounds__(BP_THREADS, (bp_waves_per_simd<T, KIND>())) void bp
     for (int i = tid; i < a.nc; i += BP_THREADS) cd[i] = a.cdeg[i];
     // the port range of the thread's variables, constant over iterations and
     // codewords: held in registers (no offset-table round trip per iteration)
-    int vp0[VJ], vd[VJ];
-    uint32_t vs01[VJ];  // message slots of the first two ports, packed
+    // (first port | degree << 16; nports <= 65535 and degrees < 2^16 by bp_launch)
+    constexpr bool R0 = !LEAN && VJ <= 4;  // first two ports' slots in registers too
+    uint32_t vpd[VJ];
+    uint32_t vs01[R0 ? VJ : 1];  // message slots of the first two ports, packed
 #pragma unroll
     for (int j = 0; j < VJ; ++j) {
         const int v = tid + j * BP_THREADS;
-        vp0[j] = v < a.nv ? (int)a.voff[v] : 0;
-        vd[j] = v < a.nv ? (int)a.voff[v + 1] - vp0[j] : 0;
-        vs01[j] = 0u;
-        if constexpr (!LEAN) {
-            const uint32_t s0 = vd[j] > 0 ? (uint32_t)a.port_slot[vp0[j]] : 0u;
-            const uint32_t s1 = vd[j] > 1 ? (uint32_t)a.port_slot[vp0[j] + 1] : 0u;
+        const int p0 = v < a.nv ? (int)a.voff[v] : 0;
+        const int d = v < a.nv ? (int)a.voff[v + 1] - p0 : 0;
+        vpd[j] = (uint32_t)p0 | ((uint32_t)d << 16);
+        if constexpr (R0) {
+            const uint32_t s0 = d > 0 ? (uint32_t)a.port_slot[p0] : 0u;
+            const uint32_t s1 = d > 1 ? (uint32_t)a.port_slot[p0 + 1] : 0u;
             vs01[j] = s0 | (s1 << 16);
         }
     }
@@ -261,18 +274,18 @@ __global__ __launch_bounds__(BP_THREADS, (bp_waves_per_simd<T, KIND>())) void bp
             for (int j = 0; j < VJ; ++j) {
                 const int v = tid + j * BP_THREADS;
                 if (v >= a.nv) continue;
-                const int p0 = vp0[j], d = vd[j];
+                const int p0 = (int)(vpd[j] & 0xffffu), d = (int)(vpd[j] >> 16);
                 T acc = chv[j];
                 if constexpr (BP_VU == 2) {
                     // two ports per round: their table and message reads issued
                     // together (one LDS round trip per round instead of per port);
                     // a round may read one padded table entry past d, which is not
                     // used; acc takes the ports in order (c_ldpc.c:171-178).  The
-                    // check-degree <= 8 kernels take the first round's slots from
-                    // registers (vs01): C3 +10 %, but the high-degree (lean)
-                    // kernels measured slower with it
-                    constexpr bool R0 = !LEAN;
-                    const int s0 = (int)(vs01[j] & 0xffffu), s1 = (int)(vs01[j] >> 16);
+                    // check-degree <= 8 kernels at 4 variables a thread take the
+                    // first round's slots from registers (vs01): C3 +10 %, but the
+                    // high-degree (lean) kernels measured slower with it
+                    const int s0 = R0 ? (int)(vs01[R0 ? j : 0] & 0xffffu) : 0;
+                    const int s1 = R0 ? (int)(vs01[R0 ? j : 0] >> 16) : 0;
                     T m0 = T(0), m1 = T(0);  // (only this thread touches its ports' slots in this pass)
                     if constexpr (R0) {
                         m0 = msg[s0];
@@ -308,9 +321,24 @@ __global__ __launch_bounds__(BP_THREADS, (bp_waves_per_simd<T, KIND>())) void bp
             __syncthreads();
             // ---- check pass (c_ldpc.c:183-194)
             int unsat = 0;
-            for (int c = tid; c < a.nc; c += BP_THREADS) {
-                if constexpr (LEAN) unsat |= check_update_lean<T, KIND>(msg, scr, c, a.nc, cd[c], a.factor) ? 1 : 0;
-                else unsat |= check_update<T, KIND, MAXDC>(msg, c, a.nc, cd[c], a.factor) ? 1 : 0;
+            if constexpr (LEAN) {
+                for (int c = tid; c < a.nc; c += BP_THREADS)
+                    unsat |= check_update_lean<T, KIND>(msg, scr, c, a.nc, cd[c], a.factor) ? 1 : 0;
+            } else if constexpr (KIND != SG_MINSUM || VJ > 4) {  // (two checks' arrays would spill)
+                for (int c = tid; c < a.nc; c += BP_THREADS)
+                    unsat |= check_update<T, KIND, MAXDC>(msg, c, a.nc, cd[c], a.factor) ? 1 : 0;
+            } else {
+                // min-sum: two checks per round, both checks' messages read before
+                // either update (their LDS round trips overlap)
+                for (int c = tid; c < a.nc; c += 2 * BP_THREADS) {
+                    const int c1 = c + BP_THREADS;
+                    const int d0 = cd[c], d1 = c1 < a.nc ? cd[c1] : 0;
+                    T L0[MAXDC], L1[MAXDC];
+                    check_load<T, MAXDC>(msg, c, a.nc, d0, L0);
+                    check_load<T, MAXDC>(msg, c1, a.nc, d1, L1);
+                    unsat |= check_update_from<T, KIND, MAXDC>(msg, c, a.nc, d0, a.factor, L0) ? 1 : 0;
+                    if (d1 > 0) unsat |= check_update_from<T, KIND, MAXDC>(msg, c1, a.nc, d1, a.factor, L1) ? 1 : 0;
+                }
             }
             if (!__syncthreads_or(unsat)) break;  // c_ldpc.c:196-197
         }
