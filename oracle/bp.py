@@ -122,3 +122,55 @@ def lxfb(L, corr=1, use_ref=False):
     f = ref_lib().Lxfb if use_ref else oracle_lib().or_lxfb
     agg = f(L.ctypes.data_as(_dp), len(L), int(corr))
     return agg, L
+
+
+def minsum_numpy(ch, vdeg, cdeg, intrlv, max_it, factor, dtype=np.float32):
+    """Flooding min-sum (c_ldpc.c:339-381 with the corrected message index of
+    :364; Lxfb(corr=0) in its min / sign-parity form, c_ldpc.c:294-314) in
+    `dtype`, vectorised over the codewords: the variable sums in port order
+    (:171-178), one multiply of every check output by the factor (:370-371),
+    the stopping rule of :196-197.  Returns (app[B, N], it int32[B]).  In
+    float64 it equals or_decode_batch("minsum") bit for bit; in float32 it is
+    the arithmetic of the GPU's single-precision kernel."""
+    ch = np.asarray(ch, dtype=dtype)
+    vdeg, cdeg, intrlv = (np.asarray(a, dtype=np.int64) for a in (vdeg, cdeg, intrlv))
+    B, N = ch.shape
+    Nc = len(cdeg)
+    vstart = np.concatenate([[0], np.cumsum(vdeg)[:-1]])
+    cstart = np.concatenate([[0], np.cumsum(cdeg)[:-1]])
+    msg = np.zeros((B, len(intrlv)), dtype)
+    f = dtype(factor)
+    app = np.zeros((B, N), dtype)
+    its = np.full(B, max_it, np.int32)
+    live = np.ones(B, bool)
+    vk = [(np.nonzero(vdeg > k)[0], intrlv[vstart[vdeg > k] + k]) for k in range(int(vdeg.max()))]
+    ck = [(np.nonzero(cdeg > k)[0], cstart[cdeg > k] + k) for k in range(int(cdeg.max()))]
+    for it in range(max_it):
+        acc = ch.copy()
+        for v, idx in vk:  # c_ldpc.c:171-178, ports in order
+            acc[:, v] = acc[:, v] + msg[:, idx]
+        for v, idx in vk:
+            msg[:, idx] = acc[:, v] - msg[:, idx]
+        app[live] = acc[live]
+        L = np.full((B, Nc, int(cdeg.max())), np.inf, dtype)
+        for k, (c, idx) in enumerate(ck):
+            L[:, c, k] = msg[:, idx]
+        a = np.abs(L)
+        sb = np.signbit(L)
+        i1 = np.argmin(a, axis=2)  # first minimum (strict '<' in the loop)
+        m1 = np.take_along_axis(a, i1[..., None], 2)[..., 0]
+        a2 = a.copy()
+        np.put_along_axis(a2, i1[..., None], np.inf, 2)
+        m2 = a2.min(axis=2)
+        sall = np.bitwise_xor.reduce(sb, axis=2)
+        unsat = sall | ~(m1 > 0)
+        for k, (c, idx) in enumerate(ck):
+            mag = np.where(i1[:, c] == k, m2[:, c], m1[:, c])
+            neg = sall[:, c] ^ sb[:, c, k]
+            msg[:, idx] = np.where(neg, -mag, mag) * f
+        done = live & ~unsat.any(axis=1)
+        its[done] = it
+        live &= ~done
+        if not live.any():
+            break
+    return app, its

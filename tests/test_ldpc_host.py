@@ -178,3 +178,24 @@ def test_oracle_under_sanitizers(tmp_path, std, rate, z):
         eapp, eit = bp.decode_batch(kind, ch, c.vdeg, c.cdeg, c.intrlv, max_it, factor)
         assert np.array_equal(it, eit), kind
         np.testing.assert_allclose(app, eapp, rtol=1e-12, atol=1e-12, err_msg=kind)
+
+
+def test_numpy_minsum_restatement_pinned(oracle_built):
+    """oracle/bp.py minsum_numpy (the float32 checker of the GPU's
+    single-precision min-sum) run in float64 equals the C restatement bit for
+    bit: on a QC code and on an irregular graph with degree-1 variables."""
+    rng = np.random.default_rng(2)
+    c = code("802.11n", "1/2", 27)
+    X = c.encode_batch(rng.integers(0, 2, (12, c.K)))
+    ch = 2 * ((1 - 2 * X) + 0.9 * rng.standard_normal(X.shape)) / 0.81
+    graphs = [(c.vdeg, c.cdeg, c.intrlv, ch)]
+    vdeg = np.array([(1, 2, 3, 5, 11, 2, 4)[v % 7] for v in range(210)], dtype=np.int64)
+    E = int(vdeg.sum())
+    cdeg = np.full(E // 6, 6, dtype=np.int64)
+    cdeg[: E - cdeg.sum()] += 1
+    graphs.append((vdeg, cdeg, rng.permutation(E).astype(np.int64), 1.0 + 2.0 * rng.standard_normal((12, 210))))
+    for vd, cd, il, y in graphs:
+        for mi in (1, 6, 40):
+            app, it = bp.minsum_numpy(y, vd, cd, il, mi, 0.7, np.float64)
+            oapp, oit = bp.decode_batch("minsum", y, vd, cd, il, mi, 0.7)
+            assert np.array_equal(it, oit) and np.array_equal(app, oapp)
