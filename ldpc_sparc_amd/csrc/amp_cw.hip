@@ -475,22 +475,39 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
             // maximum, sums without the (first) maximum (amp_fused.hip az_stage2)
             const uint16_t *sg = tb.seg + (size_t)m2 * (Lb + 1);
             const int a = sg[tl], b = sg[tl + 1];
+            // two independent online chains (even / odd entries), merged at the
+            // end: half the serial exp latency per round
             constexpr int RC = 16;
-            float m = -INFINITY, S1 = 0.f, S2 = 0.f;
+            float m = -INFINITY, S1 = 0.f, S2 = 0.f, mo = -INFINITY, S1o = 0.f, S2o = 0.f;
+            auto step = [&](float &mm, float &T1, float &T2, float xi) {
+                const bool up = xi > mm;
+                const float dlt = up ? (mm - xi) : (xi - mm);
+                const float ex = __expf(dlt * inv_tau);
+                T1 = up ? (T1 + 1.f) * ex : T1 + ex;
+                T2 = up ? (T2 + 1.f) * (ex * ex) : T2 + ex * ex;
+                mm = up ? xi : mm;
+            };
             for (int c = a; c < b; c += RC) {
                 float x[RC];
 #pragma unroll
                 for (int i = 0; i < RC; ++i) x[i] = dr[fpad(c + i)];  // inside the LDS image; masked below
 #pragma unroll
-                for (int i = 0; i < RC; ++i)
-                    if (c + i < b) {
-                        const bool up = x[i] > m;
-                        const float dlt = up ? (m - x[i]) : (x[i] - m);
-                        const float ex = __expf(dlt * inv_tau);
-                        S1 = up ? (S1 + 1.f) * ex : S1 + ex;
-                        S2 = up ? (S2 + 1.f) * (ex * ex) : S2 + ex * ex;
-                        m = up ? x[i] : m;
-                    }
+                for (int i = 0; i < RC; i += 2) {
+                    if (c + i < b) step(m, S1, S2, x[i]);
+                    if (c + i + 1 < b) step(mo, S1o, S2o, x[i + 1]);
+                }
+            }
+            if (mo > -INFINITY) {  // the odd chain into the even one (same merge as below)
+                if (mo > m) {
+                    const float f = __expf((m - mo) * inv_tau);
+                    S1 = (S1 + 1.f) * f + S1o;
+                    S2 = (S2 + 1.f) * (f * f) + S2o;
+                    m = mo;
+                } else {
+                    const float f = __expf((mo - m) * inv_tau);
+                    S1 += (1.f + S1o) * f;
+                    S2 += (1.f + S2o) * (f * f);
+                }
             }
             if (m > -INFINITY) {  // merge into the section's running statistics
                 if (m > Mr) {
