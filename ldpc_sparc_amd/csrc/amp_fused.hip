@@ -541,8 +541,9 @@ __global__ __launch_bounds__(1024) void reg_ctrl0(RegTables<T> tb, RegBufs<T> bf
         const T b = (T)red[0];
         const cx<T> *X = bf.xn + (size_t)cw * tb.nT * tb.nKmax;
         // reg_ab_out for CO outputs per thread at a time: every table load of
-        // the round issued before the dependent X gathers
-        constexpr int CO = 8;
+        // the round issued before the dependent X gathers (8 spilled at the
+        // 1024-thread register limit: 24 VGPRs in f32, 150 in f64)
+        constexpr int CO = sizeof(T) == 8 ? 2 : 4;
         for (int i0 = tid; i0 < tb.n; i0 += CO * nthr) {
             T r[CO], yv[CO], zv[CO];
 #pragma unroll
