@@ -163,6 +163,48 @@ size_t cw_lds_bytes(int img, int nslots) { return (size_t)img * 4 + (size_t)nslo
         if (tb.tprof && threadIdx.x == 0) tb.tprof[(size_t)blockIdx.x * 32 + (k)] = __builtin_readcyclecounter(); \
     } while (0)
 
+// Ab accumulation of one class: X[slot] += w_N2^(m2 k) Y[k1] for the thread's
+// slots.  The image and the X slots are disjoint LDS regions; saying so
+// (restrict) lets the compiler issue the slots' reads together instead of one
+// read-modify-write round trip after the other.
+template <int KT>
+__device__ __forceinline__ void cw_accumulate(const cx<float> *__restrict__ img, cx<float> *__restrict__ xs,
+                                              cx<float> *xr, const uint32_t *kt, const cx<float> *w, int tl) {
+    // slot j + 1's reads are issued before slot j's write (a two-deep pipeline:
+    // the compiler keeps LDS reads and writes in program order here)
+    auto ld = [&](int j, cx<float> &T, cx<float> &x) {
+        T = img[fsw(kt[j] & (CW_P - 1))];
+        x = j < CW_KL ? xs[j * CW_THREADS + tl] : xr[j < CW_KL ? 0 : j - CW_KL];
+    };
+    cx<float> Tn, xn;
+    ld(0, Tn, xn);
+#pragma unroll
+    for (int j = 0; j < KT; ++j) {  // invalid slots accumulate into themselves, unused
+        const cx<float> Tv = Tn;
+        cx<float> x = xn;
+        if (j + 1 < KT) ld(j + 1 < KT ? j + 1 : j, Tn, xn);
+        x = cmac_pk(x, Tv, w[j]);
+        if (j < CW_KL) xs[j * CW_THREADS + tl] = x;
+        else xr[j < CW_KL ? 0 : j - CW_KL] = x;
+    }
+}
+
+// Az rows of one class: the thread's rows of sum_k G[k] conj(w_N2^(m2 k)) into
+// the zeroed image (disjoint from the G slots: restrict, as above)
+template <int KT>
+__device__ __forceinline__ void cw_rows(const cx<float> *__restrict__ gs, cx<float> *__restrict__ img,
+                                        const cx<float> *xr, const uint32_t *kt, const cx<float> *w, int tl) {
+    cx<float> u{0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < KT; ++j) {
+        if (!(kt[j] & CW_VALID)) continue;
+        const cx<float> gv = j < CW_KL ? gs[j * CW_THREADS + tl] : xr[j < CW_KL ? 0 : j - CW_KL];
+        if (kt[j] & CW_NEWROW) u = {0.f, 0.f};
+        u = cmacc_pk(u, gv, w[j]);  // G conj(w_N2^(m2 k))
+        if (kt[j] & CW_ENDROW) img[fsw(kt[j] & (CW_P - 1))] = u;
+    }
+}
+
 template <int KT>
 __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float> bf, AmpScalars sc, AmpParams pr,
                                                       int t) {
@@ -237,14 +279,7 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
                 cx<float> w[KT];
 #pragma unroll
                 for (int j = 0; j < KT; ++j) w[j] = cw_w(tb, (uint32_t)m2 * (kt[j] & CW_KMASK));
-#pragma unroll
-                for (int j = 0; j < KT; ++j) {  // invalid slots accumulate into themselves, unused
-                    const cx<float> Tv = d[fsw(kt[j] & (CW_P - 1))];
-                    cx<float> x = j < CW_KL ? Xl[j * CW_THREADS + tl] : Xr[j < CW_KL ? 0 : j - CW_KL];
-                    x = cmac_pk(x, Tv, w[j]);
-                    if (j < CW_KL) Xl[j * CW_THREADS + tl] = x;
-                    else Xr[j < CW_KL ? 0 : j - CW_KL] = x;
-                }
+                cw_accumulate<KT>(d, Xl, Xr, kt, w, tl);
             }
             __syncthreads();
             if (m2 == 2) CW_TP(12);
@@ -418,17 +453,7 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
         for (int j = 0; j < KT; ++j) w[j] = cw_w(tb, (uint32_t)m2 * (kt[j] & CW_KMASK));
         __syncthreads();
         if (m2 == 2) CW_TP(17);
-        {
-            cx<float> u{0.f, 0.f};
-#pragma unroll
-            for (int j = 0; j < KT; ++j) {
-                if (!(kt[j] & CW_VALID)) continue;
-                const cx<float> gv = j < CW_KL ? Xl[j * CW_THREADS + tl] : Xr[j < CW_KL ? 0 : j - CW_KL];
-                if (kt[j] & CW_NEWROW) u = {0.f, 0.f};
-                u = cmacc_pk(u, gv, w[j]);  // G conj(w_N2^(m2 k))
-                if (kt[j] & CW_ENDROW) d[fsw(kt[j] & (CW_P - 1))] = u;
-            }
-        }
+        cw_rows<KT>(Xl, d, Xr, kt, w, tl);
         __syncthreads();
         if (m2 == 2) CW_TP(18);
         const int q0 = tb.cls_ptr[m2], q1 = tb.cls_ptr[m2 + 1];
