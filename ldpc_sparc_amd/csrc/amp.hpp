@@ -173,6 +173,7 @@ struct CwTables {
     float inv_n2;             // 1 / N2
     int img;                  // LDS reals of the FFT / class image (>= z / phi)
     const uint32_t *kt;       // [KT][1024] owned needed index k | flags; X / G slot j * 1024 + tid
+    const uint16_t *cmask;    // [Q + 1][1024] image values written per thread (class m2; rows: Q)
     const int32_t *oa, *ob;   // [n] slots of the forward outputs' X[a], X[b]
     const cx<float> *oc;      // [n][2]
     const int32_t *gi;        // [KT * 1024][4] inverse inputs by slot (output row index; unused: 0)

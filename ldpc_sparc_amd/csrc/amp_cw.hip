@@ -93,14 +93,28 @@ __device__ __forceinline__ void cw_swap32(cx<float> &a, cx<float> &b) {
 // and l ^ 32, lane half H holding inputs m = 8 H + jj (x[j + 512 m]).  A
 // radix-2 step across the halves (two rounds of permlane32 swaps) and a
 // radix-8 DFT in registers give lane half H the outputs 2 q + H, stored at
-// j 16 + 2 q + H like stockham1_stage_ct's.
+// j 16 + 2 q + H like stockham1_stage_ct's.  With CW_MASKIN the image is not
+// zeroed before the class scatter / row writes: bit 2 jj + c of msk says
+// whether component c of value jj was written for this transform (host
+// table, capi_amp.cpp build_cw), and the stale ones read as zero.
+#ifndef CW_MASKIN
+#define CW_MASKIN 1
+#endif
 template <bool INV>
-__device__ __forceinline__ void cw_stage0_r16(cx<float> *d, int tid) {
+__device__ __forceinline__ void cw_stage0_r16(cx<float> *d, int tid, uint32_t msk) {
     const int l = tid & 63, H = l >> 5, j = ((tid >> 6) << 5) | (l & 31);
     cx<float> v[8];
     const int jp = fsw(j);  // adding multiples of 256 commutes with the swizzle
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) v[jj] = d[jp + ((8 * H + jj) << 9)];
+    if constexpr (CW_MASKIN) {
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {  // all-ones / zero from the sign-extended bit
+            const uint32_t mx = (uint32_t)((int)(msk << (31 - 2 * jj)) >> 31);
+            const uint32_t my = (uint32_t)((int)(msk << (30 - 2 * jj)) >> 31);
+            v[jj] = {__uint_as_float(__float_as_uint(v[jj].x) & mx), __uint_as_float(__float_as_uint(v[jj].y) & my)};
+        }
+    }
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) cw_swap32(v[jj], v[jj + 4]);  // lane half H: x[J], x[8 + J], J = jj + 4 H
     {
@@ -127,9 +141,10 @@ __device__ __forceinline__ void cw_stage0_r16(cx<float> *d, int tid) {
 // w_{Ns R}^(e k) from the hardware sine / cosine instead of a table: no
 // global loads between its barriers.
 template <bool INV, int ST>
-__device__ __forceinline__ void cw_fft_from(cx<float> *d, int tid) {
+__device__ __forceinline__ void cw_fft_from(cx<float> *d, int tid, uint32_t msk = 0xffffu) {
+    static_assert(!CW_MASKIN || cw_radix(0) == 16, "the masked first stage is the radix-16 one");
     if constexpr (ST == 0 && cw_radix(0) == 16) {
-        cw_stage0_r16<INV>(d, tid);
+        cw_stage0_r16<INV>(d, tid, msk);
         cw_fft_from<INV, 1>(d, tid);
     } else if constexpr (ST < cw_nstages()) {
         constexpr int R = cw_radix(ST), LNS = cw_log2ns(ST);
@@ -190,7 +205,7 @@ __device__ __forceinline__ void cw_accumulate(const cx<float> *__restrict__ img,
 }
 
 // Az rows of one class: the thread's rows of sum_k G[k] conj(w_N2^(m2 k)) into
-// the zeroed image (disjoint from the G slots: restrict, as above)
+// the image (disjoint from the G slots: restrict, as above)
 template <int KT>
 __device__ __forceinline__ void cw_rows(const cx<float> *__restrict__ gs, cx<float> *__restrict__ img,
                                         const cx<float> *xr, const uint32_t *kt, const cx<float> *w, int tl) {
@@ -246,7 +261,8 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
         for (int m2 = 0; m2 < tb.Q; ++m2) {
             const int tl = cw_opaque(tid);
             if (m2 == 2) CW_TP(8);
-            for (int i = tl; i < CW_P * 8 / 16; i += CW_THREADS) reinterpret_cast<uint4 *>(smem)[i] = uint4{0, 0, 0, 0};
+            if constexpr (!CW_MASKIN)
+                for (int i = tl; i < CW_P * 8 / 16; i += CW_THREADS) reinterpret_cast<uint4 *>(smem)[i] = uint4{0, 0, 0, 0};
             float bm[CW_SN], bi[CW_SN];
 #pragma unroll
             for (int i = 0; i < CW_SN; ++i) {
@@ -254,15 +270,16 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
                 bm[i] = stM[l];
                 bi[i] = stI[l];
             }
-            __syncthreads();
+            if constexpr (!CW_MASKIN) __syncthreads();  // (masked: the previous class's closing barrier)
             if (m2 == 2) CW_TP(9);
 #pragma unroll
             for (int i = 0; i < CW_SN; ++i)
                 if (q0 + tl + i * CW_THREADS < q1)  // beta = eta(s), sparc.py:429-432
                     dr[e[i] & 0xffffu] = __expf((v[i] - bm[i]) * inv_tp) * bi[i];
+            const uint32_t cmk = CW_MASKIN ? tb.cmask[m2 * CW_THREADS + tl] : 0xffffu;  // under the barrier
             __syncthreads();
             if (m2 == 2) CW_TP(10);
-            cw_fft_from<false, 0>(d, tl);
+            cw_fft_from<false, 0>(d, tl, cmk);
             if (m2 == 2) CW_TP(11);
             if (m2 + 1 < tb.Q) {  // the next class in flight under the accumulation
                 const int tn = cw_opaque(tl);
@@ -447,17 +464,20 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
     for (int m2 = 0; m2 < tb.Q; ++m2) {
         const int tl = cw_opaque(tid);
         if (m2 == 2) CW_TP(16);
-        for (int i = tl; i < CW_P * 8 / 16; i += CW_THREADS) reinterpret_cast<uint4 *>(smem)[i] = uint4{0, 0, 0, 0};
+        // the rows' image values (the same every class; reloaded, not held across the loop)
+        const uint32_t rmk = CW_MASKIN ? tb.cmask[tb.Q * CW_THREADS + tl] : 0xffffu;
+        if constexpr (!CW_MASKIN)
+            for (int i = tl; i < CW_P * 8 / 16; i += CW_THREADS) reinterpret_cast<uint4 *>(smem)[i] = uint4{0, 0, 0, 0};
         cx<float> w[KT];
 #pragma unroll
         for (int j = 0; j < KT; ++j) w[j] = cw_w(tb, (uint32_t)m2 * (kt[j] & CW_KMASK));
-        __syncthreads();
+        if constexpr (!CW_MASKIN) __syncthreads();  // (masked: the previous class's closing barrier)
         if (m2 == 2) CW_TP(17);
         cw_rows<KT>(Xl, d, Xr, kt, w, tl);
         __syncthreads();
         if (m2 == 2) CW_TP(18);
         const int q0 = tb.cls_ptr[m2], q1 = tb.cls_ptr[m2 + 1];
-        cw_fft_from<true, 0>(d, tl);
+        cw_fft_from<true, 0>(d, tl, rmk);
         if (m2 == 2) CW_TP(19);
         float bm[CW_SN], bi[CW_SN];
 #pragma unroll

@@ -67,6 +67,7 @@ struct sg_amp_plan {
     bool no_cw = false;
     sg_amp_plan *alt = nullptr;
     uint32_t *c_kt = nullptr;
+    uint16_t *c_cmask = nullptr;  // [Q + 1][1024] per-codeword engine: written image values per thread
     int32_t *c_oa = nullptr, *c_ob = nullptr, *c_gi = nullptr;
     void *c_gc = nullptr, *c_stw = nullptr;
     // block engine (several transforms per column block, amp_block.hip)
@@ -289,7 +290,8 @@ static AmpBufs<T> bufs(const sg_amp_plan *p, int B, const void *y) {
 // owns at most KT indices; slot (j, tid) at j * 1024 + tid.
 static int build_cw(sg_amp_plan *p, const std::vector<int32_t> &row_k1, const std::vector<int32_t> &kptr,
                     const std::vector<int32_t> &kk2, const std::vector<int32_t> &oa, const std::vector<int32_t> &ob,
-                    const std::vector<int32_t> &gi, const std::vector<cd> &gc) {
+                    const std::vector<int32_t> &gi, const std::vector<cd> &gc, const std::vector<int32_t> &cls_ptr,
+                    const std::vector<uint32_t> &cls_ls) {
     const int nr = (int)row_k1.size(), nk = kptr[nr];
     if (nk > 14 * CW_THREADS) return SG_OK;  // 12 slots per thread in LDS beside the image, 2 in registers
     std::vector<int> rows(nr);
@@ -356,6 +358,28 @@ static int build_cw(sg_amp_plan *p, const std::vector<int32_t> &row_k1, const st
             lns += ilog2(R);
         }
     }
+    // Which image values the class scatter (Ab, class m2 < Q) and the row
+    // writes (Az, entry Q) leave behind, as bits of the thread that reads them
+    // in the first FFT stage (amp_cw.hip cw_stage0_r16: thread of complex
+    // index m1 = j + 512 g reads it as value g & 7, bit 2 (g & 7) + component),
+    // so that stage masks stale values instead of the image being zeroed.
+    const int Q = p->rQ;
+    std::vector<uint16_t> cmask((size_t)(Q + 1) * CW_THREADS, 0);
+    auto mbit = [&](int m2, int m1, int c) {
+        const int j = m1 & 511, g = m1 >> 9;
+        const int tid = ((j >> 5) << 6) | ((g >> 3) << 5) | (j & 31);
+        cmask[(size_t)m2 * CW_THREADS + tid] |= (uint16_t)(1u << (2 * (g & 7) + c));
+    };
+    for (int m2 = 0; m2 < Q; ++m2)
+        for (int q = cls_ptr[m2]; q < cls_ptr[m2 + 1]; ++q) {
+            const int loc = (int)(cls_ls[q] & 0xffffu);
+            mbit(m2, fsw(loc >> 1), loc & 1);  // fsw is its own inverse
+        }
+    for (int r = 0; r < nr; ++r) {
+        mbit(Q, row_k1[r], 0);
+        mbit(Q, row_k1[r], 1);
+    }
+    SG_TRY(upload(p, &p->c_cmask, cmask));
     SG_TRY(upload(p, &p->c_kt, kt));
     SG_TRY(upload(p, &p->c_oa, c_oa));
     SG_TRY(upload(p, &p->c_ob, c_ob));
@@ -598,7 +622,7 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
     SG_TRY(upload_cx(p, &p->r_twb, twb));
     if (p->precision == SG_F32 && nT == 1 && P == (1 << 13) && Lblk <= CW_THREADS && n <= 8 * CW_THREADS &&
         Q <= 64 && p->rmaxcls <= 9 * CW_THREADS && p->rimg == 2 * P && fpad(p->rmaxcls + 16) < p->rimg)
-        SG_TRY(build_cw(p, row_k1[0], kptr[0], kk2[0], f_oa, f_ob, f_gi, f_gc));
+        SG_TRY(build_cw(p, row_k1[0], kptr[0], kk2[0], f_oa, f_ob, f_gi, f_gc, cls_ptr, cls_ls));
     return SG_OK;
 }
 
@@ -629,6 +653,7 @@ static CwTables ctables(const sg_amp_plan *p) {
     tb.L = p->L; tb.M = p->M; tb.LM = p->LM; tb.n = p->n; tb.N2 = p->N2; tb.Q = p->rQ; tb.Lblk = p->Lblk;
     tb.KT = p->cwKT; tb.log2P = p->rlog2P; tb.maxcls = p->rmaxcls; tb.maxseg = p->rmaxseg;
     tb.img = p->rimg;
+    tb.cmask = p->c_cmask;
     tb.kt = p->c_kt; tb.oa = p->c_oa; tb.ob = p->c_ob; tb.oc = (const cx<float> *)p->r_oc;
     tb.gi = p->c_gi; tb.gc = (const cx<float> *)p->c_gc;
     tb.cls_ptr = p->r_cls_ptr; tb.cls_ls = p->r_cls_ls; tb.qpos = p->r_qpos; tb.seg = p->r_seg;
