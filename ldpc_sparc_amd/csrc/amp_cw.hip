@@ -258,18 +258,26 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
             v[i] = s[q];
             e[i] = tb.cls_ls[q];
         }
-        for (int m2 = 0; m2 < tb.Q; ++m2) {
-            const int tl = cw_opaque(tid);
-            if (m2 == 2) CW_TP(8);
-            if constexpr (!CW_MASKIN)
-                for (int i = tl; i < CW_P * 8 / 16; i += CW_THREADS) reinterpret_cast<uint4 *>(smem)[i] = uint4{0, 0, 0, 0};
-            float bm[CW_SN], bi[CW_SN];
+        // section max and 1/sum of the class's entries; with CW_MASKIN those of
+        // class m2 + 1 are gathered before class m2's closing barrier (not with
+        // register-held slots: <14> then spills 12 VGPRs)
+        constexpr bool early = CW_MASKIN && KT <= CW_KL;
+        float bm[CW_SN], bi[CW_SN];
+        auto gather_stats = [&]() {
 #pragma unroll
             for (int i = 0; i < CW_SN; ++i) {
                 const int l = e[i] >> 16;
                 bm[i] = stM[l];
                 bi[i] = stI[l];
             }
+        };
+        if constexpr (early) gather_stats();
+        for (int m2 = 0; m2 < tb.Q; ++m2) {
+            const int tl = cw_opaque(tid);
+            if (m2 == 2) CW_TP(8);
+            if constexpr (!CW_MASKIN)
+                for (int i = tl; i < CW_P * 8 / 16; i += CW_THREADS) reinterpret_cast<uint4 *>(smem)[i] = uint4{0, 0, 0, 0};
+            if constexpr (!early) gather_stats();
             if constexpr (!CW_MASKIN) __syncthreads();  // (masked: the previous class's closing barrier)
             if (m2 == 2) CW_TP(9);
 #pragma unroll
@@ -298,6 +306,7 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
                 for (int j = 0; j < KT; ++j) w[j] = cw_w(tb, (uint32_t)m2 * (kt[j] & CW_KMASK));
                 cw_accumulate<KT>(d, Xl, Xr, kt, w, tl);
             }
+            if (early && m2 + 1 < tb.Q) gather_stats();
             __syncthreads();
             if (m2 == 2) CW_TP(12);
         }
@@ -466,6 +475,13 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
         if (m2 == 2) CW_TP(16);
         // the rows' image values (the same every class; reloaded, not held across the loop)
         const uint32_t rmk = CW_MASKIN ? tb.cmask[tb.Q * CW_THREADS + tl] : 0xffffu;
+        float bm[CW_SN], bi[CW_SN];  // section max, 1/sum: gathered under the rows and the transform
+#pragma unroll
+        for (int i = 0; i < CW_SN; ++i) {
+            const int l = e[i] >> 16;
+            bm[i] = have_beta ? stM[l] : 0.f;
+            bi[i] = have_beta ? stI[l] : 0.f;
+        }
         if constexpr (!CW_MASKIN)
             for (int i = tl; i < CW_P * 8 / 16; i += CW_THREADS) reinterpret_cast<uint4 *>(smem)[i] = uint4{0, 0, 0, 0};
         cx<float> w[KT];
@@ -479,13 +495,6 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
         const int q0 = tb.cls_ptr[m2], q1 = tb.cls_ptr[m2 + 1];
         cw_fft_from<true, 0>(d, tl, rmk);
         if (m2 == 2) CW_TP(19);
-        float bm[CW_SN], bi[CW_SN];
-#pragma unroll
-        for (int i = 0; i < CW_SN; ++i) {
-            const int l = e[i] >> 16;
-            bm[i] = have_beta ? stM[l] : 0.f;
-            bi[i] = have_beta ? stI[l] : 0.f;
-        }
         float snv[CW_SN];
 #pragma unroll
         for (int i = 0; i < CW_SN; ++i) {
