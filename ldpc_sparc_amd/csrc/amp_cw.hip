@@ -475,13 +475,6 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
         if (m2 == 2) CW_TP(16);
         // the rows' image values (the same every class; reloaded, not held across the loop)
         const uint32_t rmk = CW_MASKIN ? tb.cmask[tb.Q * CW_THREADS + tl] : 0xffffu;
-        float bm[CW_SN], bi[CW_SN];  // section max, 1/sum: gathered under the rows and the transform
-#pragma unroll
-        for (int i = 0; i < CW_SN; ++i) {
-            const int l = e[i] >> 16;
-            bm[i] = have_beta ? stM[l] : 0.f;
-            bi[i] = have_beta ? stI[l] : 0.f;
-        }
         if constexpr (!CW_MASKIN)
             for (int i = tl; i < CW_P * 8 / 16; i += CW_THREADS) reinterpret_cast<uint4 *>(smem)[i] = uint4{0, 0, 0, 0};
         cx<float> w[KT];
@@ -495,6 +488,13 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
         const int q0 = tb.cls_ptr[m2], q1 = tb.cls_ptr[m2 + 1];
         cw_fft_from<true, 0>(d, tl, rmk);
         if (m2 == 2) CW_TP(19);
+        float bm[CW_SN], bi[CW_SN];
+#pragma unroll
+        for (int i = 0; i < CW_SN; ++i) {
+            const int l = e[i] >> 16;
+            bm[i] = have_beta ? stM[l] : 0.f;
+            bi[i] = have_beta ? stI[l] : 0.f;
+        }
         float snv[CW_SN];
 #pragma unroll
         for (int i = 0; i < CW_SN; ++i) {
