@@ -495,6 +495,12 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
             bm[i] = have_beta ? stM[l] : 0.f;
             bi[i] = have_beta ? stI[l] : 0.f;
         }
+        int sa = 0, sb = 0;  // the section's segment of the class, read under the s update
+        if (tl < Lb) {
+            const uint16_t *sg = tb.seg + (size_t)m2 * (Lb + 1);
+            sa = sg[tl];
+            sb = sg[tl + 1];
+        }
         float snv[CW_SN];
 #pragma unroll
         for (int i = 0; i < CW_SN; ++i) {
@@ -527,8 +533,7 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
         if (tl < Lb) {
             // partial of section tl over its segment of the class: running
             // maximum, sums without the (first) maximum (amp_fused.hip az_stage2)
-            const uint16_t *sg = tb.seg + (size_t)m2 * (Lb + 1);
-            const int a = sg[tl], b = sg[tl + 1];
+            const int a = sa, b = sb;
             // two independent online chains (even / odd entries), merged at the
             // end: half the serial exp latency per round
             constexpr int RC = 16;
