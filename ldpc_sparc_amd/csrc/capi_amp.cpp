@@ -6,6 +6,7 @@
 #include <cmath>
 #include <complex>
 #include <memory>
+#include <random>
 #include <type_traits>
 #include <vector>
 
@@ -285,9 +286,73 @@ static AmpBufs<T> bufs(const sg_amp_plan *p, int B, const void *y) {
     return bf;
 }
 
+// Bank-aware placement of the rows on the threads (amp_cw.hip cw_accumulate:
+// at slot j, lanes 0-31 and 32-63 of a wavefront each read one image value
+// at fsw(k1) with ds_read_b64, whose bank pair is fsw(k1) mod 32; distinct
+// rows on one bank pair serialise).  Local search from the load-balanced
+// placement: swap two rows of the same length that start at the same slot of
+// threads in different lane groups when the summed worst bank multiplicity
+// of the cells they touch does not grow.  Deterministic (fixed seed); the
+// slot structure of every thread is unchanged.
+#ifndef CW_BANKBAL
+#define CW_BANKBAL 1
+#endif
+static void cw_bank_balance(std::vector<std::vector<int>> &own, const std::vector<int32_t> &row_k1,
+                            const std::vector<int32_t> &kptr, int KT) {
+    const int T = CW_THREADS;
+    std::vector<int> at((size_t)T * KT, -1), pos((size_t)T * KT, -1), start((size_t)T * KT, 0);
+    for (int t = 0; t < T; ++t) {  // row / list position at each slot; rows start where flagged
+        int j = 0;
+        for (int i = 0; i < (int)own[t].size(); ++i) {
+            const int r = own[t][i], len = kptr[r + 1] - kptr[r];
+            start[(size_t)t * KT + j] = len;
+            for (int q = 0; q < len; ++q, ++j) {
+                at[(size_t)t * KT + j] = r;
+                pos[(size_t)t * KT + j] = i;
+            }
+        }
+    }
+    auto addr = [&](int t, int j) { const int r = at[(size_t)t * KT + j]; return r < 0 ? 0 : fsw(row_k1[r]); };
+    auto cell = [&](int g, int j) {  // LDS cycles of the 32 lanes' reads at slot j (distinct addresses per bank pair)
+        int a[32], cnt[32] = {0}, worst = 0;
+        for (int l = 0; l < 32; ++l) {
+            a[l] = addr(g * 32 + l, j);
+            bool dup = false;
+            for (int m = 0; m < l && !dup; ++m) dup = a[m] == a[l];
+            if (!dup) worst = std::max(worst, ++cnt[a[l] & 31]);
+        }
+        return worst;
+    };
+    // candidates by (start slot, length)
+    std::vector<std::vector<int>> by((size_t)KT * (KT + 1));
+    for (int t = 0; t < T; ++t)
+        for (int j = 0; j < KT; ++j)
+            if (const int len = start[(size_t)t * KT + j]) by[(size_t)j * (KT + 1) + len].push_back(t);
+    std::mt19937 rng(12345);
+    const int iters = 8 * T * KT;
+    for (int it = 0; it < iters; ++it) {
+        const int A = (int)(rng() % T), j = (int)(rng() % KT), len = start[(size_t)A * KT + j];
+        if (!len) continue;
+        const auto &cand = by[(size_t)j * (KT + 1) + len];
+        const int B = cand[rng() % cand.size()];
+        const int gA = A / 32, gB = B / 32;
+        if (gA == gB) continue;
+        int before = 0, after = 0;
+        for (int q = j; q < j + len; ++q) before += cell(gA, q) + cell(gB, q);
+        for (int q = j; q < j + len; ++q) std::swap(at[(size_t)A * KT + q], at[(size_t)B * KT + q]);
+        for (int q = j; q < j + len; ++q) after += cell(gA, q) + cell(gB, q);
+        if (after > before) {
+            for (int q = j; q < j + len; ++q) std::swap(at[(size_t)A * KT + q], at[(size_t)B * KT + q]);
+            continue;
+        }
+        std::swap(own[A][pos[(size_t)A * KT + j]], own[B][pos[(size_t)B * KT + j]]);
+    }
+}
+
 // Per-codeword engine tables (amp_cw.hip): the needed indices of each row go
 // to one thread (longest rows first, to the least loaded thread), so a thread
-// owns at most KT indices; slot (j, tid) at j * 1024 + tid.
+// owns at most KT indices; slot (j, tid) at j * 1024 + tid; then
+// cw_bank_balance.
 static int build_cw(sg_amp_plan *p, const std::vector<int32_t> &row_k1, const std::vector<int32_t> &kptr,
                     const std::vector<int32_t> &kk2, const std::vector<int32_t> &oa, const std::vector<int32_t> &ob,
                     const std::vector<int32_t> &gi, const std::vector<cd> &gc, const std::vector<int32_t> &cls_ptr,
@@ -314,6 +379,9 @@ static int build_cw(sg_amp_plan *p, const std::vector<int32_t> &row_k1, const st
     }
     if (KT > 14) return SG_OK;  // the staged engine only
     KT = KT <= 12 ? 12 : 14;   // kernel instances (cw_iter<12>: all slots in LDS; <14>: two in registers)
+#if CW_BANKBAL
+    cw_bank_balance(own, row_k1, kptr, KT);
+#endif
     const int P = p->rP, n = p->n;
     std::vector<uint32_t> kt((size_t)KT * CW_THREADS, 0u);
     std::vector<int32_t> cmap(nk, 0);
