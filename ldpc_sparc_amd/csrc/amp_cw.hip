@@ -530,6 +530,10 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
         }
         __syncthreads();
         if (m2 == 2) CW_TP(21);
+        // wavefronts with a segment longer than one round run at raised issue
+        // priority: they set the time of the closing barrier
+        const bool long_wave = __ballot(tl < Lb && sb - sa > 16) != 0;
+        if (long_wave) __builtin_amdgcn_s_setprio(2);
         if (tl < Lb) {
             // partial of section tl over its segment of the class: running
             // maximum, sums without the (first) maximum (amp_fused.hip az_stage2)
@@ -582,6 +586,7 @@ __global__ __launch_bounds__(CW_THREADS) void cw_iter(CwTables tb, RegBufs<float
             }
             if (jt >= q0 && jt < q1) s_true = dr[fpad(jt - q0)];
         }
+        if (long_wave) __builtin_amdgcn_s_setprio(0);
         if (m2 == 2) CW_TP(22);
         __syncthreads();  // the next class overwrites the image
         if (m2 == 2) CW_TP(23);
