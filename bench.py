@@ -106,11 +106,36 @@ def guard_env():
         sys.exit(3)
 
 
+def _visible_list(var):
+    v = os.environ.get(var)
+    if v is None:
+        return None
+    return [x for x in v.split(",") if x.strip() != ""]
+
+
 def visible_gpus():
-    """GPUs this process could use, counted without initialising the GPU
-    (torch.cuda.device_count() does not initialise HIP on this image)."""
-    import torch
-    return int(torch.cuda.device_count())
+    """GPUs this process could use, counted through amdsmi (the kernel
+    driver's view) without any HIP call, so the launcher parent never
+    initialises the GPU: torch.cuda.device_count() goes through amdsmi too on
+    this image but falls back to hipGetDeviceCount when amdsmi fails, which
+    would initialise HIP here.  The *_VISIBLE_DEVICES masks narrow the count.
+    If amdsmi cannot count, the launcher refuses (exit 2) rather than guess."""
+    try:
+        import amdsmi
+        amdsmi.amdsmi_init(amdsmi.AmdSmiInitFlags.INIT_AMD_GPUS)
+        try:
+            n = len(amdsmi.amdsmi_get_processor_handles())
+        finally:
+            amdsmi.amdsmi_shut_down()
+    except Exception as e:  # no driver, no library: refuse, never fall back to a HIP call
+        sys.stderr.write(f"bench.py: cannot count GPUs through amdsmi ({type(e).__name__}: "
+                         f"{str(e).strip().splitlines()[-1] if str(e).strip() else ''}); refusing to launch\n")
+        sys.exit(2)
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        lst = _visible_list(var)
+        if lst is not None:
+            n = min(n, len(lst))
+    return n
 
 
 def maybe_spawn(args):

@@ -283,7 +283,8 @@ int sg_amp_plan_info(const sg_amp_plan *p, int *w, int *nT, int *Mr, int *Mc, in
  * decoder; returns the engine or a negative error code. */
 int sg_amp_plan_engine(const sg_amp_plan *p, int B);
 /* What the last decode through this plan ran: *engine as sg_amp_plan_engine
- * (-1 before any decode), *handover_iter the first iteration the per-codeword
+ * (-1 before any decode and after a decode call with B = 0 or one that failed
+ * before choosing an engine: every decode call resets it), *handover_iter the first iteration the per-codeword
  * engine left to the staged engine (-1: no hand-over), *on_companion 1 when
  * the decode ran on the P = 16384 companion plan (may be NULL). */
 int sg_amp_last_decode(const sg_amp_plan *p, int *engine, int *handover_iter, int *on_companion);

@@ -1394,10 +1394,23 @@ int sg_amp_plan_info(const sg_amp_plan *p, int *w, int *nT, int *Mr, int *Mc, in
     return SG_OK;
 }
 
+// sg_amp_last_decode reports what the latest decode call ran: reset at the
+// entry of every decode, so a call that returns early (B == 0) or fails
+// partway reports engine -1 instead of a previous call's engine and hand-over
+static void reset_last(sg_amp_plan *p) {
+    for (sg_amp_plan *q : {p, p->alt}) {
+        if (!q) continue;
+        q->last_ran = nullptr;
+        q->last_engine = -1;
+        q->last_handover = -1;
+    }
+}
+
 int sg_amp_decode_device(sg_amp_plan *p, const void *d_y, int B, const int32_t *d_true_idx, double awgn_var,
                          int t_max, double rtol, int phi_method, int32_t *d_map_idx, int32_t *d_t_final,
                          double *d_nmse, double *d_psi, void *stream) {
     SG_CHECK_ARG(p, "plan is NULL");
+    reset_last(p);
     SG_CHECK_ARG(t_max > 1, "t_max must be > 1 (sparc.py:168)");
     SG_CHECK_ARG(rtol > 0 && rtol < 1, "rtol must be in (0, 1)");
     SG_CHECK_ARG(phi_method == 1 || phi_method == 2, "phi_est_method must be 1 or 2");
@@ -1419,6 +1432,7 @@ int sg_amp_decode_device(sg_amp_plan *p, const void *d_y, int B, const int32_t *
 int sg_amp_decode(sg_amp_plan *p, const double *y, int B, const int32_t *true_idx, double awgn_var, int t_max,
                   double rtol, int phi_method, int32_t *map_idx, int32_t *t_final, double *nmse, double *psi) {
     SG_CHECK_ARG(p, "plan is NULL");
+    reset_last(p);
     SG_CHECK_ARG(B >= 0, "negative batch");
     if (B == 0) return SG_OK;
     SG_CHECK_ARG(y && map_idx && t_final && nmse && psi, "null host buffer");

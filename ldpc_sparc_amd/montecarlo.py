@@ -73,7 +73,7 @@ def _first_reaching(cum, need):
 
 
 def run_point(trial, point, *, block, blocks_per_round, rank, world, agg, min_errors=None, max_units=None,
-              checkpoint_dir=None, tag="campaign", params=None):
+              checkpoint_dir=None, tag="campaign", params=None, max_rounds=None):
     """Run one point until `min_errors` frame errors or `max_units` units
     (globally).  trial(point, first_block, n_blocks, block) -> int64[NC]
     counters of the blocks [first_block, first_block + n_blocks).
@@ -88,7 +88,9 @@ def run_point(trial, point, *, block, blocks_per_round, rank, world, agg, min_er
 
     `params` (campaign parameters) is stored in the checkpoint; resuming with
     different parameters raises ValueError instead of adding up counts of
-    different experiments."""
+    different experiments.  `max_rounds` ends this call after that many rounds
+    without marking the point done (an interrupted run; the checkpoint lets a
+    later call continue it)."""
     total = np.zeros(NC, dtype=np.int64)
     next_block = 0
     done = False
@@ -105,7 +107,11 @@ def run_point(trial, point, *, block, blocks_per_round, rank, world, agg, min_er
             next_block = int(st["next_block"])
             done = bool(st.get("done", False))
     per_unit = getattr(trial, "per_unit", False)
+    rounds = 0
     while not done:
+        if max_rounds is not None and rounds >= max_rounds:
+            break
+        rounds += 1
         if min_errors is not None and total[2] >= min_errors:
             break
         if max_units is not None and total[0] >= max_units:
@@ -311,31 +317,45 @@ class ConcatTrial:
 
 def concat_ber_sweep(L, M, n, P, L_unprotected, mults, ebn0_db, *, codewords, block=256, blocks_per_round=None,
                      rank=0, world=1, agg=None, design_seed=0, seed=0, t_max=25, bp_its=200, precision="f32",
-                     ldpc=("802.11n", "1/2", 81), min_errors=None, checkpoint_dir=None, npz_file=None, rng="device"):
+                     ldpc=("802.11n", "1/2", 81), min_errors=None, checkpoint_dir=None, npz_file=None, rng="device",
+                     trial=None, max_rounds=None):
     """BER / FER of concatenated SPARC + LDPC against Eb/N0 (the experiment of
     ldpc_sparc/performance_plots_general.py:100-138 for the plain concatenated
     decoder), `codewords` per point sharded over the ranks.  Eb/N0 to noise as
     the bench: awgn_var = P / (2 R_overall 10^(Eb/N0 / 10)), R_overall = user
     bits / n.  Returns one dict per point; rank 0 writes `npz_file` in the
     layout of performance_plots_general.py:138 (ber_store_averages, _max,
-    _min over the blocks rank 0 decoded, and snr_store = Eb/N0 in dB)."""
-    from .pipeline import ConcatPipeline
+    _min over the blocks rank 0 decoded, and snr_store = Eb/N0 in dB).
+    `trial(point, first_block, n_blocks, block)` (counters as ConcatTrial's)
+    replaces the GPU pipeline (CPU rehearsals: tools/c5_sweep.py --rehearsal); `max_rounds`
+    interrupts every point after that many rounds (run_point)."""
+    from .ldpc import code
     agg = agg or Aggregator()
-    pipe = ConcatPipeline(L, M, n, P, L_unprotected, mults, ldpc=ldpc, design_seed=design_seed,
-                          precision=precision, t_max=t_max, bp_its=bp_its)
-    user_bits = L_unprotected * pipe.logM + mults * pipe.c.K
+    logM = int(np.log2(M))
+    user_bits = L_unprotected * logM + mults * code(*ldpc).K
     r_overall = user_bits / n
     vars_ = [P / (2 * r_overall * 10 ** (e / 10)) for e in ebn0_db]
-    trial = ConcatTrial(pipe, vars_, seed, rng)
+    if trial is None:
+        from .pipeline import ConcatPipeline
+        pipe = ConcatPipeline(L, M, n, P, L_unprotected, mults, ldpc=ldpc, design_seed=design_seed,
+                              precision=precision, t_max=t_max, bp_its=bp_its)
+        assert pipe.L_unp * pipe.logM + pipe.mults * pipe.c.K == user_bits
+        trial = ConcatTrial(pipe, vars_, seed, rng)
     bpr = blocks_per_round or max(1, world)
     out = []
     for point, e in enumerate(ebn0_db):
+        params = {"P": P, "L_unprotected": L_unprotected, "mults": mults, "ebn0_db": float(e),
+                  "seed": seed, "design_seed": design_seed, "t_max": t_max, "bp_its": bp_its,
+                  "precision": precision, "ldpc": list(ldpc), "codewords": codewords, "rng": rng,
+                  "min_errors": min_errors}
+        if min_errors is not None:
+            # the counters stop at round granularity, so with an error target
+            # the round size is part of the experiment (without one the point
+            # ends at `codewords`, a multiple of the block, at any round size)
+            params["blocks_per_round"] = bpr
         tot = run_point(trial, point, block=block, blocks_per_round=bpr, rank=rank, world=world, agg=agg,
                         min_errors=min_errors, max_units=codewords, checkpoint_dir=checkpoint_dir,
-                        tag=f"concat_L{L}_M{M}_n{n}",
-                        params={"P": P, "L_unprotected": L_unprotected, "mults": mults, "ebn0_db": float(e),
-                                "seed": seed, "design_seed": design_seed, "t_max": t_max, "bp_its": bp_its,
-                                "precision": precision, "ldpc": list(ldpc), "codewords": codewords, "rng": rng})
+                        tag=f"concat_L{L}_M{M}_n{n}", params=params, max_rounds=max_rounds)
         out.append({"ebn0_db": float(e), "awgn_var": vars_[point], "codewords": int(tot[0]),
                     "ber": float(tot[1]) / (tot[0] * user_bits) if tot[0] else None,
                     "fer": float(tot[2]) / tot[0] if tot[0] else None,
@@ -343,7 +363,7 @@ def concat_ber_sweep(L, M, n, P, L_unprotected, mults, ebn0_db, *, codewords, bl
                     "R_overall": r_overall})
     if npz_file and rank == 0:
         avg = np.array([[o["ber"] for o in out]], dtype=float)
-        bb = [trial.block_ber.get(p, [np.nan]) for p in range(len(ebn0_db))]
+        bb = [getattr(trial, "block_ber", {}).get(p, [np.nan]) for p in range(len(ebn0_db))]
         np.savez(npz_file, ber_store_averages=avg, ber_store_max=np.array([[np.max(b) for b in bb]]),
                  ber_store_min=np.array([[np.min(b) for b in bb]]), snr_store=np.asarray(ebn0_db, dtype=float))
     return out

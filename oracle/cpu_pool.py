@@ -11,8 +11,10 @@ restatements out over such a pool:
     the min-sum loop index corrected), a chunk of codewords per task.
 
 Used by bench.py's cpu_baseline legs and by tests/ as the checker.  The
-product never imports it.  Workers start with the 'spawn' method before the
-parent touches anything, so no child inherits GPU state.
+product never imports it.  Workers start with the 'spawn' method: each is a
+fresh interpreter that imports only numpy/scipy and the oracle, so no child
+inherits GPU state even though the parent (bench.py's CPU legs) has already
+initialised and used the GPU when it builds the pool.
 """
 import multiprocessing as mp
 import os

@@ -53,6 +53,56 @@ def test_more_gpus_than_visible_refused():
     assert r.returncode == 2 and "GPU" in r.stderr
 
 
+_LAUNCH_PROBE = r'''
+import subprocess, sys, types
+fake = types.ModuleType("amdsmi")
+class _F:
+    INIT_AMD_GPUS = 1
+fake.AmdSmiInitFlags = _F
+fake.amdsmi_init = lambda flags: None
+fake.amdsmi_get_processor_handles = lambda: list(range(8))
+fake.amdsmi_shut_down = lambda: None
+sys.modules["amdsmi"] = fake
+calls = []
+class _R:
+    returncode = 0
+subprocess.run = lambda cmd, env=None: (calls.append(cmd), _R())[1]
+sys.argv = ["bench.py", "--gpus", "8"]
+import bench
+code = None
+try:
+    bench.maybe_spawn(bench.parse())
+except SystemExit as e:
+    code = e.code
+import json
+print(json.dumps({"code": code, "torch_loaded": "torch" in sys.modules,
+                  "hip_loaded": any("amdhip" in l for l in open("/proc/self/maps")),
+                  "cmd": calls[0] if calls else None}))
+'''
+
+
+def test_launcher_counts_gpus_without_hip():
+    """--gpus 8 with 8 GPUs visible (amdsmi stubbed): the parent starts
+    torch.distributed.run with 8 processes per node and exits with its code,
+    without importing torch or mapping the HIP runtime (so no GPU call can
+    precede the launch)."""
+    env = {k: v for k, v in _env().items() if not k.endswith("_VISIBLE_DEVICES")}
+    r = subprocess.run([sys.executable, "-c", _LAUNCH_PROBE], env=env, capture_output=True, text=True,
+                       timeout=120, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["code"] == 0 and not out["torch_loaded"] and not out["hip_loaded"], out
+    assert "torch.distributed.run" in out["cmd"] and "--nproc-per-node=8" in out["cmd"]
+
+
+def test_visible_devices_mask_narrows_count():
+    r = subprocess.run([sys.executable, "-c", _LAUNCH_PROBE], env=_env(HIP_VISIBLE_DEVICES="0,1"),
+                       capture_output=True, text=True, timeout=120, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["code"] == 2 and out["cmd"] is None, out
+
+
 def test_cpu_pool_matches_serial_oracle():
     """Two-process pool = the serial CPU restatement, codeword for codeword."""
     from oracle import bp, cpu_pool, sparc_ref

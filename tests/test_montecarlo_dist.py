@@ -2,6 +2,7 @@
 the counter all-reduce (gloo, world_size 2, the same code path that uses RCCL
 between GPUs), invariance of a campaign's result to the number of ranks,
 checkpoint/resume, and the results.txt -> CSV conversion of results2csv.c."""
+import json
 import os
 import socket
 
@@ -178,3 +179,39 @@ def test_results_csv_format():
     assert mc.results_to_csv([line]) == ["11, 0.5, 0, 81, 1.7134, 400000, 91, 388800000, 8741, 6220937"]
     line = ('802.16', '2/3', 3, 'B', -1.3103816364765377, 100, 100, 4800, 1439, 20000)
     assert mc.results_to_csv([line]) == ["16, 0.666667, 1, 3, -1.31038, 100, 100, 4800, 1439, 20000"]
+
+
+def _c5_rehearsal(world, ckpt, extra=()):
+    """tools/c5_sweep.py --rehearsal at `world` ranks (torch.distributed.run,
+    gloo on the CPU); the JSON lines rank 0 prints."""
+    import subprocess
+    import sys
+    tool = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "c5_sweep.py")
+    args = ["--rehearsal", "--ebn0", "1", "3", "4.5", "6", "--codewords", "40960", "--block", "256",
+            "--blocks-per-round", "8", "--min-errors", "3000", "--checkpoint", ckpt] + list(extra)
+    if world == 1:
+        cmd = [sys.executable, tool] + args
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+               "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", tool] + args
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_c5_sweep_rehearsal_world8_kill_and_resume(tmp_path):
+    """The C5 sweep driver at 8 ranks (gloo rehearsal of the RCCL path):
+    interrupted after 2 rounds of every point, then resumed from rank 0's
+    checkpoints, it ends with the same per-point counts as one uninterrupted
+    rank; the interrupted run stopped short of them."""
+    one = _c5_rehearsal(1, str(tmp_path / "one"))
+    part = _c5_rehearsal(8, str(tmp_path / "eight"), ["--max-rounds", "2"])
+    full = _c5_rehearsal(8, str(tmp_path / "eight"))
+    keys = ("codewords", "ber", "fer", "unprotected_bit_errors", "protected_bit_errors")
+    assert [[p[k] for k in keys] for p in full[:-1]] == [[p[k] for k in keys] for p in one[:-1]]
+    assert full[-1]["gpus"] == 8 and full[-1]["rehearsal"]
+    assert any(p["codewords"] < f["codewords"] for p, f in zip(part[:-1], full[:-1]))
+    assert all(p["codewords"] <= 2 * 8 * 256 for p in part[:-1])
+    # the error target ends the low-Eb/N0 points early; the high ones run to the codeword cap
+    assert full[0]["codewords"] < 40960 and full[-2]["codewords"] == 40960
