@@ -362,6 +362,15 @@ def amp_cpu_baseline(st, args, seconds, procs):
     csec, gsec = (cmap != t), (g != t)
     nb = nd * L * st["logM"]
     iters = int(ctf.sum())
+    # codewords outside t_final +-2 that the GPU stopped where the reference's
+    # own relative psi change was within 10 % of rtol (a threshold stop)
+    dtf = gtf[done] - ctf
+    thr = 0
+    for k, b in enumerate(done):
+        if dtf[k] < -2:
+            ps = res[b][3]
+            tg = int(gtf[b])
+            thr += int(abs(ps[tg - 1] - ps[tg - 2]) / abs(ps[tg - 2]) <= 1.1e-6)
     return {"value": nd / el, "unit": "codewords/s", "cores": procs, "kind": "port",
             "sample": f"{nd} of the {B} C2 codewords the GPU decoded (R={args.rate}, t_max={args.t_max}, {iters} AMP "
                       f"iterations, {el:.1f} s wall) by oracle/sparc_ref.py (numpy/scipy fftpack DCT, float128 "
@@ -374,6 +383,9 @@ def amp_cpu_baseline(st, args, seconds, procs):
                           "identical_codeword_decisions": float((cmap == g).all(1).mean()),
                           "t_final_equal": float((ctf == gtf[done]).mean()),
                           "t_final_max_abs_diff": int(np.abs(ctf - gtf[done]).max()),
+                          "t_final_within_2": float((np.abs(dtf) <= 2).mean()),
+                          "outside_2_at_reference_threshold": thr,
+                          "outside_2_unexplained": int((np.abs(dtf) > 2).sum()) - thr,
                           "note": "the GPU's decisions for the same received words (f32 engine vs the f64/"
                                   "float128 CPU restatement), over every codeword of the CPU sample"}}
 

@@ -72,7 +72,8 @@ int sg_device_synchronize(void);
  * launch count per phase (arrays of SG_PH_COUNT) and resets the counters. */
 enum sg_phase {
     SG_PH_AB_A = 0, SG_PH_AB_B = 1, SG_PH_AZ_A = 2, SG_PH_AZ_B = 3, SG_PH_ETA = 4,
-    SG_PH_CONTROL = 5, SG_PH_BP = 6, SG_PH_DENSE = 7, SG_PH_AMP_CW = 8, SG_PH_COUNT = 9
+    SG_PH_CONTROL = 5, SG_PH_BP = 6, SG_PH_DENSE = 7, SG_PH_AMP_CW = 8, SG_PH_CW2_AB = 9, SG_PH_CW2_AZ = 10,
+    SG_PH_CW2_CTRL = 11, SG_PH_COUNT = 12
 };
 int sg_profile_enable(int on);
 int sg_profile_collect(double *total_ms, int64_t *launches);

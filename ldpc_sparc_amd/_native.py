@@ -140,7 +140,7 @@ SG_INT_NAIVE, SG_INT_NAIVE_POST, SG_INT_DIFF, SG_INT_DIFF_POST = 0, 1, 2, 3
 INTEGRATED_MODES = {"naive": SG_INT_NAIVE, "naive_posteriors": SG_INT_NAIVE_POST, "integrated": SG_INT_DIFF,
                     "integrated_posteriors": SG_INT_DIFF_POST}
 
-SG_PH_COUNT = 9
+SG_PH_COUNT = 12
 
 
 def lib():

@@ -186,6 +186,37 @@ struct CwTables {
     uint64_t *tprof;          // diagnostics (SG_AMP_TPROF): [B][32] shader-clock stamps, or null
 };
 size_t cw_lds_bytes(int img, int nslots);
+
+// Split per-codeword engine (amp_cw2.hip): each codeword's AMP iteration as
+// two 512-thread workgroups (the two halves of the Q classes), two
+// workgroups per CU, so one workgroup's barrier waits and memory latency
+// overlap the other's work.  Four launches per iteration: Ab halves (partial
+// H of every output, in registers), control (residual, phi, tau, z/phi),
+// Az halves (rows, inverse transform, s update, partial section statistics),
+// merge.  Output-owned: thread tid owns the outputs of slots j * 512 + tid,
+// j < OT, grouped by conjugate row pair {r, P - r} of the P-point stage (host
+// build_cw2).  See DESIGN.md "Split per-codeword engine".
+constexpr int CW2_THREADS = 512;
+constexpr uint32_t CW_SELF = 1u << 23;  // the pair's two rows coincide (r = 0 or P / 2)
+struct Cw2Tables {
+    int L, M, LM, n, N2, Q, Lblk, OT, maxcls;
+    float inv_n2;             // 1 / N2
+    const uint32_t *cmask;    // [Q + 1][512] image values each thread's first FFT stage reads (class m2; rows: Q)
+    const uint32_t *ka;       // [OT][512] a | CW_VALID | CW_NEWROW (first of its pair) | CW_ENDROW | CW_SELF
+    const int32_t *oi;        // [OT][512] output index (invalid slots: 0)
+    const float4 *cf;         // [OT][512] (c1, c2): output = Re(c1 H[a] + c2 conj H[N2 - a])
+    const float4 *gf;         // [OT][512] (al, be): G[a] += al z/phi, G[N2 - a] += be z/phi
+    const int32_t *cls_ptr;   // [Q+1]
+    const uint32_t *cls_ls;   // [Mc] padded real LDS index | section << 16
+    const int32_t *qpos;      // [Mc]
+    const uint16_t *seg;      // [Q][Lblk+1]
+    float4 *xp;               // [B][2][OT][512] partial (H[a], conj H[b]) of each half
+    float *vz;                // [B][OT][512] z / phi in slot order
+    float4 *part;             // [B][2][Lblk] partial section statistics (max, R1, R2, s of the true entry or NaN)
+    uint64_t *tprof;          // diagnostics (SG_AMP_TPROF): [2 B][64] shader-clock stamps (Ab 0-31, Az 32-63), or null
+};
+int cw2_launch_iter(const Cw2Tables &tb, const RegBufs<float> &bf, const AmpScalars &sc, const AmpParams &pr, int t,
+                    hipStream_t s);
 int cw_launch_iter(const CwTables &tb, const RegBufs<float> &bf, const AmpScalars &sc, const AmpParams &pr, int t,
                    hipStream_t s);
 

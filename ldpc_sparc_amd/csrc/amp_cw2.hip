@@ -1,0 +1,618 @@
+// Split per-codeword AMP engine on gfx950 (the C2 headline path).  One AMP
+// iteration of the regular design (sparc.py:883-999 with the sub-sampled DCT
+// operators of sub_dct, sparc.py:648-701) per codeword as four launches:
+//
+//   cw2_ab    (2 B workgroups)  half h of the Q classes: beta of the class
+//             (from s and the section statistics) -> LDS scatter -> P-point
+//             FFT -> for every output i owned by the thread:
+//                 H[a]      += W Y_m2[r],
+//                 conj H[b] += W conj Y_m2[P - r],   W = w_N2^(m2 a), r = a mod P
+//             in registers; the two halves' partials go to xp.
+//   cw2_ctrl  (B)  z = y - Re(c1 H[a] + c2 conj H[b]) + b z, phi, tau
+//             (sparc.py:931-969); z / phi in slot order (vz).
+//   cw2_az    (2 B)  half h of the classes: rows r and P - r of each owned
+//             conjugate pair from the outputs' al z/phi conj(W) and be z/phi W
+//             -> inverse P-point FFT -> s = beta_prev + tau u (sparc.py:972) in
+//             class order -> per-section partial (max, sums without the max).
+//   cw2_merge (B)  the two halves' section statistics -> max, 1/sum, psi,
+//             NMSE, early stop (sparc.py:973-988).
+//
+// Why split: with one 1024-thread workgroup per CU (amp_cw.hip) every phase of
+// a class is separated by workgroup barriers and nothing overlaps them (SQ:
+// ~42 % of wave cycles waiting).  Here each codeword's classes are shared by
+// two 512-thread workgroups with 64 KB of LDS each, two per CU, so one
+// workgroup's barriers, LDS latency and global loads run beside the other's
+// transform.  The needed spectrum no longer lives in LDS: the forward output
+// Re(c1 H[a] + c2 conj H[N2 - a]) and the inverse input of output i touch
+// only the conjugate row pair {a mod P, P - a mod P} of the P-point stage, so
+// a thread that owns whole pairs accumulates H[a] and conj H[b] of its
+// outputs in registers (one twiddle per output and class, no X slots in LDS,
+// no read-modify-write), and writes the pair's rows without conflicts.
+//
+// The P-point transform (P = 8192) runs at 16 values per thread in three
+// LDS passes: radix 32 (each butterfly shared by lanes l and l ^ 32 through
+// v_permlane32_swap, no twiddles), then radix 16 twice with twiddles from the
+// hardware sine / cosine.
+#include "amp.hpp"
+
+namespace sg {
+namespace {
+
+constexpr int C2_T = CW2_THREADS;
+constexpr int C2_LOG2P = 13, C2_P = 1 << C2_LOG2P, C2_EPT = C2_P / C2_T;  // 16 values per thread
+constexpr int C2_SC = 9;   // class entries per thread and chunk
+constexpr int C2_NC = 2;   // chunks: a class holds at most C2_SC * C2_NC * 512 = 9216 entries
+static_assert(C2_EPT == 16, "the transform is written for 16 values per thread");
+
+__device__ __forceinline__ int c2_opaque(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+// w_N2^j = exp(-2 pi i j / N2) from the hardware sine / cosine (revolutions;
+// (j mod N2) / N2 is exact in f32 for N2 <= 2^19)
+__device__ __forceinline__ cx<float> c2_w(const Cw2Tables &tb, uint32_t j) {
+    const float x = (float)(j & (uint32_t)(tb.N2 - 1)) * tb.inv_n2;
+    return {__builtin_amdgcn_cosf(x), -__builtin_amdgcn_sinf(x)};
+}
+
+// lanes 32..63 of a <-> lanes 0..31 of b (v_permlane32_swap, no LDS)
+__device__ __forceinline__ void c2_swap32(cx<float> &a, cx<float> &b) {
+    const auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.x), __float_as_uint(b.x), false, false);
+    const auto ry = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.y), __float_as_uint(b.y), false, false);
+    a = {__uint_as_float(rx[0]), __uint_as_float(ry[0])};
+    b = {__uint_as_float(rx[1]), __uint_as_float(ry[1])};
+}
+
+// First Stockham stage at radix 32 (Ns = 1, no twiddles), 16 values per
+// thread: butterfly j = 32 w + (l & 31) of wavefront w is shared by lanes l
+// and l ^ 32, lane half H holding inputs m = 16 H + jj (x[j + 256 m]).  Two
+// rounds of permlane32 swaps around a radix-2 decimation-in-frequency step
+// (half H then holds x[J], x[J + 16] for J = jj + 8 H; a_J = x_J + x_(J+16),
+// b_J = (x_J - x_(J+16)) w32^J) give half p the 16 values of sub-sequence p,
+// whose 16-point DFT in registers is X[2 q + p]; stored at j 32 + 2 q + H.
+// The image is not zeroed before a scatter / the row writes: bit 2 jj + c of
+// msk says whether component c of value jj was written for this transform
+// (host table, build_cw2), the stale ones read as zero.
+template <bool INV>
+__device__ __forceinline__ void c2_stage0_r32(cx<float> *d, int tid, uint32_t msk) {
+    const int l = tid & 63, H = l >> 5, j = ((tid >> 6) << 5) | (l & 31);
+    cx<float> v[16];
+    const int jp = fsw(j);  // adding multiples of 256 commutes with the swizzle
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) v[jj] = d[jp + ((16 * H + jj) << 8)];
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) {  // all-ones / zero from the sign-extended bit
+        const uint32_t mx = (uint32_t)((int)(msk << (31 - 2 * jj)) >> 31);
+        const uint32_t my = (uint32_t)((int)(msk << (30 - 2 * jj)) >> 31);
+        v[jj] = {__uint_as_float(__float_as_uint(v[jj].x) & mx), __uint_as_float(__float_as_uint(v[jj].y) & my)};
+    }
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) c2_swap32(v[jj], v[jj + 8]);  // lane half H: x[J], x[16 + J], J = jj + 8 H
+    {
+        // w32^jj = cos(2 pi jj / 32) -+ i sin(2 pi jj / 32), jj < 8 (forward -, inverse +)
+        constexpr float co[8] = {1.f, 0.98078528040323044913f, 0.92387953251128675613f, 0.83146961230254523708f,
+                                 0.70710678118654752440f, 0.55557023301960222474f, 0.38268343236508977173f,
+                                 0.19509032201612826785f};
+        constexpr float si[8] = {0.f, 0.19509032201612826785f, 0.38268343236508977173f, 0.55557023301960222474f,
+                                 0.70710678118654752440f, 0.83146961230254523708f, 0.92387953251128675613f,
+                                 0.98078528040323044913f};
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+            const cx<float> u = v[jj], x16 = v[jj + 8];
+            v[jj] = cadd(u, x16);
+            const cx<float> w = {co[jj], INV ? si[jj] : -si[jj]};
+            const cx<float> t = jj == 0 ? csub(u, x16) : cmul(csub(u, x16), w);  // (u - x16) w32^jj
+            v[jj + 8] = H ? mul_mi<float, INV>(t) : t;                              // * w32^(8 H)
+        }
+    }
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) c2_swap32(v[jj], v[jj + 8]);  // lane half p: sub-sequence p, J = 0..15
+    dft16<float, INV>(v);                                        // v[q] = X_j[2 q + H]
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) d[fsw((j << 5) | (q << 1) | H)] = v[q];
+    __syncthreads();
+}
+
+// Radix-16 stage with Ns = 2^LNS (fft.hpp stockham1_stage_ct, one butterfly
+// per thread) and its stage twiddles w_(16 Ns)^(e k) from the hardware sine /
+// cosine (e = 1, 2, 3, 4, 8, 12; the others as products, fft.hpp tw_apply)
+template <bool INV, int LNS>
+__device__ __forceinline__ void c2_stage_r16(cx<float> *d, int tid) {
+    cx<float> wl[6];
+    constexpr float inv = 1.0f / (float)(1 << (LNS + 4));
+    const int k = tid & ((1 << LNS) - 1);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+        const float x = (float)((tw_exp(16, q) * k) & ((1 << (LNS + 4)) - 1)) * inv;
+        wl[q] = {__builtin_amdgcn_cosf(x), -__builtin_amdgcn_sinf(x)};
+    }
+    stockham1_stage_ct<float, INV, 16, C2_EPT, C2_LOG2P, LNS>(d, wl, tid);
+}
+
+template <bool INV>
+__device__ __forceinline__ void c2_fft(cx<float> *d, int tid, uint32_t msk) {
+    c2_stage0_r32<INV>(d, tid, msk);
+    c2_stage_r16<INV, 5>(d, c2_opaque(tid));
+    c2_stage_r16<INV, 9>(d, c2_opaque(tid));
+}
+
+}  // namespace
+
+// diagnostics (SG_AMP_TPROF): thread 0 stamps the shader clock at point k of
+// the half's third class (cw2_ab: 0-15, cw2_az: 32-47) and at kernel entry / exit
+#define C2_TP(k)                                                                                                \
+    do {                                                                                                        \
+        if (tb.tprof && threadIdx.x == 0) tb.tprof[(size_t)blockIdx.x * 64 + (k)] = __builtin_readcyclecounter(); \
+    } while (0)
+#define C2_TPC(k)                          \
+    do {                                   \
+        if (m2 == h * Qh + 2) C2_TP(k);   \
+    } while (0)
+
+// ---------------------------------------------------------------------------- Ab
+// LDS: the P-point image (64 KB), then the previous beta's section max and
+// 1/sum (stM, stI: 8 KB), staged once per launch.
+constexpr size_t C2_IMG_BYTES = (size_t)C2_P * 8;
+constexpr size_t C2_LDS_BYTES = C2_IMG_BYTES + 2 * 1024 * 4;
+constexpr int C2_SN = C2_NC * C2_SC;  // class entries per thread
+
+
+template <int OT>
+__global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> bf) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cx<float> *d = reinterpret_cast<cx<float> *>(smem);
+    float *dr = reinterpret_cast<float *>(smem);
+    float *sM = reinterpret_cast<float *>(smem + C2_IMG_BYTES), *sI = sM + 1024;
+    const int h = blockIdx.x & 1, cw = blockIdx.x >> 1, tid = threadIdx.x;
+    if (!bf.active[cw]) return;
+    const size_t lb = (size_t)cw * tb.L;
+    for (int l = tid; l < tb.L; l += C2_T) {  // previous beta's section max, 1/sum
+        sM[l] = bf.stM[lb + l];
+        sI[l] = bf.stI[lb + l];
+    }
+    const float inv_tp = (float)(1.0 / bf.tau[cw]);
+    const float *s = bf.s + (size_t)cw * tb.LM;
+    cx<float> Ha[OT], Hb[OT];  // H[a], conj H[b] of the thread's outputs over this half's classes
+#pragma unroll
+    for (int j = 0; j < OT; ++j) Ha[j] = Hb[j] = {0.f, 0.f};
+    const int Qh = tb.Q >> 1;
+    __syncthreads();  // the staged statistics
+    C2_TP(10);
+    for (int m2 = h * Qh; m2 < (h + 1) * Qh; ++m2) {
+        const int tl = c2_opaque(tid);
+        C2_TPC(0);
+        const int q0 = tb.cls_ptr[m2], q1 = tb.cls_ptr[m2 + 1];
+        float v[C2_SN];
+        uint32_t e[C2_SN];
+#pragma unroll
+        for (int i = 0; i < C2_SN; ++i) {  // every load of the class slice in one round trip
+            const int q = min(q0 + tl + i * C2_T, q1 - 1);
+            v[i] = s[q];
+            e[i] = tb.cls_ls[q];
+        }
+#pragma unroll
+        for (int c = 0; c < C2_NC; ++c) {  // beta = eta(s), sparc.py:429-432, scattered into the image
+#pragma unroll
+            for (int i = c * C2_SC; i < (c + 1) * C2_SC; ++i) {
+                const int sec = e[i] >> 16;
+                if (q0 + tl + i * C2_T < q1) dr[e[i] & 0xffffu] = __expf((v[i] - sM[sec]) * inv_tp) * sI[sec];
+            }
+            C2_TPC(1 + c);
+        }
+        const uint32_t cmk = tb.cmask[m2 * C2_T + tl];
+        __syncthreads();
+        C2_TPC(3);
+        c2_fft<false>(d, tl, cmk);
+        C2_TPC(6);
+        // H[a] += W Y[r], conj H[b] += W conj Y[P - r] (invalid slots: a = 0, unused); the
+        // owned indices a reloaded per class (L1) rather than held across the transform
+        {
+            uint32_t ka[OT];
+#pragma unroll
+            for (int j = 0; j < OT; ++j) ka[j] = tb.ka[j * C2_T + c2_opaque(tl)];
+#pragma unroll
+            for (int j = 0; j < OT; ++j) {
+                const uint32_t a = ka[j] & CW_KMASK;
+                const int r = (int)a & (C2_P - 1);
+                const cx<float> ya = d[fsw(r)], yb = d[fsw((C2_P - r) & (C2_P - 1))];
+                const cx<float> w = c2_w(tb, (uint32_t)m2 * a);
+                Ha[j] = cmac_pk(Ha[j], w, ya);
+                Hb[j] = cmacc_pk(Hb[j], w, yb);
+            }
+        }
+        C2_TPC(8);
+        __syncthreads();
+        C2_TPC(9);
+    }
+    C2_TP(11);
+    float4 *xp = tb.xp + ((size_t)cw * 2 + h) * OT * C2_T;
+#pragma unroll
+    for (int j = 0; j < OT; ++j) xp[j * C2_T + tid] = make_float4(Ha[j].x, Ha[j].y, Hb[j].x, Hb[j].y);
+}
+
+// ---------------------------------------------------------------------------- control
+__device__ __forceinline__ double c2_block_sum(double v, double *red) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    double t = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
+    return t;
+}
+
+template <int OT>
+__global__ __launch_bounds__(C2_T) void cw2_ctrl(Cw2Tables tb, RegBufs<float> bf, AmpScalars sc, AmpParams pr,
+                                                 int t) {
+    __shared__ double red[C2_T / 64];
+    const int cw = blockIdx.x, tid = threadIdx.x;
+    if (!bf.active[cw]) return;
+    const bool have_beta = t > 0;
+    double *psi = sc.psi + cw, *psi_prev = sc.psi_prev + cw;
+    float *z = bf.z + (size_t)cw * tb.n;
+    const float *y = bf.y + (size_t)cw * tb.n;
+    const bool sum_z = pr.phi_method != 1;
+    double g;
+    float bco = 0.f;
+    if (have_beta) {
+        const double ps = *psi, ph = bf.phi[cw];
+        g = pr.W[0] * ps;  // ndim 0: gamma = W psi (sparc.py:938-940)
+        if (tid == 0) {
+            *psi_prev = ps;
+            bf.tau_prev[cw] = bf.tau[cw];
+            sc.phi_prev[cw] = ph;
+            sc.gamma[cw] = g;
+            sc.bcoef[cw] = g / ph;
+        }
+        bco = (float)(g / ph);
+    } else {
+        g = pr.W[0];
+        if (tid == 0) sc.gamma[cw] = g;
+    }
+    const float4 *xp0 = tb.xp + (size_t)cw * 2 * OT * C2_T, *xp1 = xp0 + (size_t)OT * C2_T;
+    float zr[OT];
+    double acc = 0.0;
+    {
+        int oi[OT];
+        float yv[OT], zv[OT];
+#pragma unroll
+        for (int j = 0; j < OT; ++j) {  // every load issued together (invalid slots: output 0, unused)
+            oi[j] = tb.oi[j * C2_T + tid];
+            yv[j] = y[oi[j]];
+            zv[j] = have_beta ? z[oi[j]] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < OT; ++j) {
+            float zn = yv[j];
+            if (have_beta) {  // Onsager residual, sparc.py:943-946
+                const float4 x0 = xp0[j * C2_T + tid], x1 = xp1[j * C2_T + tid];
+                const float4 c = tb.cf[j * C2_T + tid];
+                const cx<float> ha = {x0.x + x1.x, x0.y + x1.y}, hb = {x0.z + x1.z, x0.w + x1.w};
+                float r = 0.f;
+                r += (c.x * ha.x - c.y * ha.y) + (c.z * hb.x - c.w * hb.y);  // Re(c1 H[a] + c2 conj H[b])
+                zn = (yv[j] - r) + bco * zv[j];
+            }
+            zr[j] = zn;
+        }
+#pragma unroll
+        for (int j = 0; j < OT; ++j) {
+            if (tb.ka[j * C2_T + tid] & CW_VALID) {
+                z[oi[j]] = zr[j];
+                if (sum_z) acc += (double)zr[j] * (double)zr[j];
+            }
+        }
+    }
+    double phi;
+    if (sum_z) {
+        phi = c2_block_sum(acc, red) / (double)tb.n;  // sparc.py:949-955
+    } else {
+        phi = pr.awgn_var + g;
+    }
+    const double tv_new = (tb.L * phi / tb.n) / pr.W[0];  // sparc.py:958-969
+    if (tid == 0) {
+        bf.phi[cw] = phi;
+        bf.tau[cw] = tv_new;
+    }
+    const float phf = (float)phi;
+    float *vz = tb.vz + (size_t)cw * OT * C2_T;
+#pragma unroll
+    for (int j = 0; j < OT; ++j) vz[j * C2_T + tid] = zr[j] / phf;  // z / phi (sparc.py:972)
+}
+
+// ---------------------------------------------------------------------------- Az
+template <int OT>
+__global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> bf, int t) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cx<float> *d = reinterpret_cast<cx<float> *>(smem);
+    float *dr = reinterpret_cast<float *>(smem);
+    float *sM = reinterpret_cast<float *>(smem + C2_IMG_BYTES), *sI = sM + 1024;
+    const int h = blockIdx.x & 1, cw = blockIdx.x >> 1, tid = threadIdx.x;
+    if (!bf.active[cw]) return;
+    const size_t lb = (size_t)cw * tb.L;
+    const bool have_beta = t > 0;
+    for (int l = tid; l < tb.L; l += C2_T) {  // previous beta's section max, 1/sum (t = 0: unused)
+        sM[l] = have_beta ? bf.stM[lb + l] : 0.f;
+        sI[l] = have_beta ? bf.stI[lb + l] : 0.f;
+    }
+    const float inv_tp = have_beta ? (float)(1.0 / bf.tau_prev[cw]) : 1.f;  // the previous beta's tau
+    const double tv = bf.tau[cw];
+    const float tau = (float)tv, inv_tau = (float)(1.0 / tv);
+    float *s = bf.s + (size_t)cw * tb.LM;
+    const float *vz = tb.vz + (size_t)cw * OT * C2_T;
+    // running statistics of sections tid and tid + 512 over this half's classes
+    const int Lb = tb.Lblk;
+    float Mr[2] = {-INFINITY, -INFINITY}, R1[2] = {0.f, 0.f}, R2[2] = {0.f, 0.f}, st[2] = {NAN, NAN};
+    int jt[2] = {-1, -1};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int sec = tid + k * C2_T;
+        if (bf.true_idx && sec < Lb) jt[k] = tb.qpos[sec * tb.M + bf.true_idx[lb + sec]];
+    }
+    const int Qh = tb.Q >> 1;
+    __syncthreads();  // the staged statistics
+    C2_TP(42);
+    for (int m2 = h * Qh; m2 < (h + 1) * Qh; ++m2) {
+        const int tl = c2_opaque(tid);
+        C2_TPC(32);
+        const uint32_t rmk = tb.cmask[tb.Q * C2_T + tl];
+        {  // rows r and P - r of each owned pair: sum of al v conj(W) / be v W over its outputs
+           // (v = z / phi, al, be and a reloaded per class from L1 / L2: held across the transform
+           // they would spill)
+            uint32_t ka[OT];
+            cx<float> g1[OT], g2[OT];
+#pragma unroll
+            for (int j = 0; j < OT; ++j) {
+                ka[j] = tb.ka[j * C2_T + tl];
+                const float4 gc = tb.gf[j * C2_T + tl];
+                const float vv = vz[j * C2_T + tl];
+                g1[j] = {gc.x * vv, gc.y * vv};
+                g2[j] = {gc.z * vv, gc.w * vv};
+            }
+            cx<float> u0{0.f, 0.f}, u1{0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < OT; ++j) {
+                const uint32_t k = ka[j];
+                if (!(k & CW_VALID)) continue;
+                const uint32_t a = k & CW_KMASK;
+                const cx<float> w = c2_w(tb, (uint32_t)m2 * a);
+                if (k & CW_NEWROW) u0 = u1 = {0.f, 0.f};
+                u0 = cmacc_pk(u0, g1[j], w);
+                u1 = cmac_pk(u1, g2[j], w);
+                if (k & CW_ENDROW) {
+                    const int r = (int)a & (C2_P - 1);
+                    if (k & CW_SELF) {
+                        d[fsw(r)] = cadd(u0, u1);
+                    } else {
+                        d[fsw(r)] = u0;
+                        d[fsw(C2_P - r)] = u1;
+                    }
+                }
+            }
+        }
+        C2_TPC(33);
+        __syncthreads();
+        C2_TPC(34);
+        c2_fft<true>(d, tl, rmk);
+        C2_TPC(35);
+        const int q0 = tb.cls_ptr[m2], q1 = tb.cls_ptr[m2 + 1];
+        float snv[C2_SN];
+        {
+            float v[C2_SN];
+            uint32_t e[C2_SN];
+#pragma unroll
+            for (int i = 0; i < C2_SN; ++i) {  // every load of the class slice in one round trip
+                const int q = min(q0 + tl + i * C2_T, q1 - 1);
+                e[i] = tb.cls_ls[q];
+                v[i] = s[q];  // (t = 0: unused)
+            }
+#pragma unroll
+            for (int i = 0; i < C2_SN; ++i) {
+                const int sec = e[i] >> 16;
+                const float b = have_beta ? __expf((v[i] - sM[sec]) * inv_tp) * sI[sec] : 0.f;
+                snv[i] = b + tau * dr[e[i] & 0xffffu];
+            }
+        }
+        int sa[2], sb[2];  // the sections' segments of the class
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int sec = tl + k * C2_T;
+            const uint16_t *sg = tb.seg + (size_t)m2 * (Lb + 1);
+            sa[k] = sec < Lb ? sg[sec] : 0;
+            sb[k] = sec < Lb ? sg[sec + 1] : 0;
+        }
+        C2_TPC(36);
+#pragma unroll
+        for (int c = 0; c < C2_SN; ++c) {  // s to HBM straight from the registers (class order)
+            const int q = q0 + tl + c * C2_T;
+            if (q < q1) s[q] = snv[c];
+        }
+        C2_TPC(37);
+        __syncthreads();
+        C2_TPC(38);
+#pragma unroll
+        for (int c = 0; c < C2_SN; ++c) {  // s of the class in class order, skewed by fpad
+            const int q = q0 + tl + c * C2_T;
+            if (q < q1) dr[fpad(q - q0)] = snv[c];
+        }
+        __syncthreads();
+        C2_TPC(39);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            // partial of the section over its segment: running maximum, sums
+            // without the (first) maximum, two online chains (even / odd entries)
+            const int a = sa[k], b = sb[k];
+            constexpr int RC = 16;
+            float m = -INFINITY, S1 = 0.f, S2 = 0.f, mo = -INFINITY, S1o = 0.f, S2o = 0.f;
+            auto step = [&](float &mm, float &T1, float &T2, float xi) {
+                const bool up = xi > mm;
+                const float dlt = up ? (mm - xi) : (xi - mm);
+                const float ex = __expf(dlt * inv_tau);
+                T1 = up ? (T1 + 1.f) * ex : T1 + ex;
+                T2 = up ? (T2 + 1.f) * (ex * ex) : T2 + ex * ex;
+                mm = up ? xi : mm;
+            };
+            for (int c = a; c < b; c += RC) {
+                float x[RC];
+#pragma unroll
+                for (int i = 0; i < RC; ++i) x[i] = dr[fpad(c + i)];  // inside the LDS image; masked below
+#pragma unroll
+                for (int i = 0; i < RC; i += 2) {
+                    if (c + i < b) step(m, S1, S2, x[i]);
+                    if (c + i + 1 < b) step(mo, S1o, S2o, x[i + 1]);
+                }
+            }
+            if (mo > -INFINITY) {
+                if (mo > m) {
+                    const float f = __expf((m - mo) * inv_tau);
+                    S1 = (S1 + 1.f) * f + S1o;
+                    S2 = (S2 + 1.f) * (f * f) + S2o;
+                    m = mo;
+                } else {
+                    const float f = __expf((mo - m) * inv_tau);
+                    S1 += (1.f + S1o) * f;
+                    S2 += (1.f + S2o) * (f * f);
+                }
+            }
+            if (m > -INFINITY) {
+                if (m > Mr[k]) {
+                    const float f = __expf((Mr[k] - m) * inv_tau);
+                    R1[k] = (R1[k] + 1.f) * f + S1;
+                    R2[k] = (R2[k] + 1.f) * (f * f) + S2;
+                    Mr[k] = m;
+                } else {
+                    const float f = __expf((m - Mr[k]) * inv_tau);
+                    R1[k] += (1.f + S1) * f;
+                    R2[k] += (1.f + S2) * (f * f);
+                }
+            }
+            if (jt[k] >= q0 && jt[k] < q1) st[k] = dr[fpad(jt[k] - q0)];
+        }
+        C2_TPC(40);
+        __syncthreads();  // the next class overwrites the image
+        C2_TPC(41);
+    }
+    C2_TP(43);
+    float4 *part = tb.part + ((size_t)cw * 2 + h) * Lb;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int sec = tid + k * C2_T;
+        if (sec < Lb) part[sec] = make_float4(Mr[k], R1[k], R2[k], st[k]);
+    }
+}
+
+// ---------------------------------------------------------------------------- merge
+__global__ __launch_bounds__(1024) void cw2_merge(Cw2Tables tb, RegBufs<float> bf, AmpScalars sc, AmpParams pr,
+                                                  int t) {
+    __shared__ double red[16];
+    const int cw = blockIdx.x, tid = threadIdx.x;
+    if (!bf.active[cw]) return;
+    const size_t lb = (size_t)cw * tb.L;
+    const int Lb = tb.Lblk;
+    const float inv_tau = (float)(1.0 / bf.tau[cw]);
+    double a = 0.0, er = 0.0;
+    if (tid < Lb) {
+        const float4 *part = tb.part + (size_t)cw * 2 * Lb;
+        float Mr = -INFINITY, R1 = 0.f, R2 = 0.f, s_true = NAN;
+        for (int h = 0; h < 2; ++h) {  // the halves in order: same merge as the class merge of cw2_az
+            const float4 p = part[h * Lb + tid];
+            const float m = p.x;
+            if (!(p.w != p.w)) s_true = p.w;
+            if (m > -INFINITY) {
+                if (m > Mr) {
+                    const float f = __expf((Mr - m) * inv_tau);
+                    R1 = (R1 + 1.f) * f + p.y;
+                    R2 = (R2 + 1.f) * (f * f) + p.z;
+                    Mr = m;
+                } else {
+                    const float f = __expf((m - Mr) * inv_tau);
+                    R1 += (1.f + p.y) * f;
+                    R2 += (1.f + p.z) * (f * f);
+                }
+            }
+        }
+        const float inv = 1.f / (1.f + R1);
+        bf.stM[lb + tid] = Mr;
+        bf.stI[lb + tid] = inv;
+        // 1 - sum beta^2 = (2 R1 + R1^2 - R2) / (1 + R1)^2, no cancellation
+        const double i2 = (double)inv * (double)inv, r1 = R1, r2 = R2;
+        a = (2.0 * r1 + r1 * r1 - r2) * i2;
+        if (bf.true_idx) {
+            if (s_true == Mr) {
+                er = (r1 * r1 + r2) * i2;
+            } else {
+                const double bt = (double)(__expf((s_true - Mr) * inv_tau) * inv);
+                er = (1.0 + r2) * i2 - 2.0 * bt + 1.0;
+            }
+        }
+    }
+    a = c2_block_sum(a, red);
+    er = c2_block_sum(er, red);
+    if (tid == 0) {
+        double *psi = sc.psi + cw, *psi_prev = sc.psi_prev + cw;
+        double *nmse = sc.nmse + (size_t)cw * pr.t_max;
+        const double denom = (double)tb.L;
+        const double pnew = a / denom;
+        *psi = pnew;
+        nmse[t + 1] = er / denom;
+        bool stop = false;
+        if (t > 0) {
+            const double pp = *psi_prev;
+            stop = fabs(pnew - pp) <= pr.atol + pr.rtol * fabs(pp);  // sparc.py:984-986
+        }
+        if (stop) {  // nmse[t:] = nmse[t] (sparc.py:985)
+            for (int tt = t + 1; tt < pr.t_max; ++tt) nmse[tt] = nmse[t];
+            sc.t_final[cw] = t + 1;
+            bf.active[cw] = 0;
+        } else if (t == pr.t_max - 2) {
+            sc.t_final[cw] = t + 1;
+            bf.active[cw] = 0;
+        }
+    }
+}
+
+template <int OT>
+static int cw2_launch(const Cw2Tables &tb, const RegBufs<float> &bf, const AmpScalars &sc, const AmpParams &pr,
+                      int t, hipStream_t s) {
+    const size_t lds = C2_LDS_BYTES;  // the P-point image (also the class copy: fpad(maxcls + 16) < 2 P), stM, stI
+    const dim3 g2(2 * bf.B), gB(bf.B);
+    if (t > 0) {
+        ProfScope ps(SG_PH_CW2_AB, s);
+        hipLaunchKernelGGL((cw2_ab<OT>), g2, dim3(C2_T), lds, s, tb, bf);
+    }
+    {
+        ProfScope ps(SG_PH_CW2_CTRL, s);
+        hipLaunchKernelGGL((cw2_ctrl<OT>), gB, dim3(C2_T), 0, s, tb, bf, sc, pr, t);
+    }
+    {
+        ProfScope ps(SG_PH_CW2_AZ, s);
+        hipLaunchKernelGGL((cw2_az<OT>), g2, dim3(C2_T), lds, s, tb, bf, t);
+    }
+    {
+        ProfScope ps(SG_PH_CW2_CTRL, s);
+        hipLaunchKernelGGL((cw2_merge), gB, dim3(1024), 0, s, tb, bf, sc, pr, t);
+    }
+    return SG_OK;
+}
+
+int cw2_launch_iter(const Cw2Tables &tb, const RegBufs<float> &bf, const AmpScalars &sc, const AmpParams &pr, int t,
+                    hipStream_t s) {
+    if (bf.B <= 0) return SG_OK;
+    if (tb.Q % 2 || tb.L > 1024 || tb.Lblk > 2 * C2_T || tb.maxcls > C2_NC * C2_SC * C2_T ||
+        fpad(tb.maxcls + 16) >= 2 * C2_P || tb.N2 != C2_P * tb.Q)
+        return fail(SG_ERR_UNSUPPORTED, "split per-codeword engine: sizes outside its compile-time bounds");
+    ProfScope ps(SG_PH_AMP_CW, s);
+    switch (tb.OT) {
+    case 12: SG_TRY(cw2_launch<12>(tb, bf, sc, pr, t, s)); break;
+    case 13: SG_TRY(cw2_launch<13>(tb, bf, sc, pr, t, s)); break;
+    case 14: SG_TRY(cw2_launch<14>(tb, bf, sc, pr, t, s)); break;
+    case 16: SG_TRY(cw2_launch<16>(tb, bf, sc, pr, t, s)); break;
+    default: return fail(SG_ERR_UNSUPPORTED, "split per-codeword engine: %d outputs per thread", tb.OT);
+    }
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
+}  // namespace sg

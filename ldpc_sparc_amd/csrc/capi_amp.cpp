@@ -68,6 +68,12 @@ struct sg_amp_plan {
     bool no_cw = false;
     sg_amp_plan *alt = nullptr;
     uint32_t *c_kt = nullptr;
+    // split per-codeword engine (amp_cw2.hip): outputs per thread (0 = not built) and its tables
+    int cw2OT = 0;
+    uint32_t *c2_ka = nullptr, *c2_cmask = nullptr;
+    int32_t *c2_oi = nullptr;
+    void *c2_cf = nullptr, *c2_gf = nullptr;
+    void *ws_c2xp = nullptr, *ws_c2vz = nullptr, *ws_c2part = nullptr;
     uint16_t *c_cmask = nullptr;  // [Q + 1][1024] per-codeword engine: written image values per thread
     int32_t *c_oa = nullptr, *c_ob = nullptr, *c_gi = nullptr;
     void *c_gc = nullptr, *c_stw = nullptr;
@@ -174,7 +180,8 @@ static int plan_free_ws(sg_amp_plan *p) {
                    (void **)&p->ws_psi, (void **)&p->ws_psi_prev, (void **)&p->ws_phi_prev, (void **)&p->ws_gamma,
                    (void **)&p->ws_bco, (void **)&p->ws_nmse, (void **)&p->ws_active, (void **)&p->ws_argmax,
                    (void **)&p->ws_true, (void **)&p->ws_tfinal, &p->ws_s, &p->ws_tu, &p->ws_xn, &p->ws_part,
-                   &p->ws_stM, &p->ws_stI, (void **)&p->ws_tau_prev, &p->ws_gbuf};
+                   &p->ws_stM, &p->ws_stI, (void **)&p->ws_tau_prev, &p->ws_gbuf, &p->ws_c2xp, &p->ws_c2vz,
+                   &p->ws_c2part};
     for (void **x : ws) {
         if (*x) hipFree(*x);
         *x = nullptr;
@@ -204,6 +211,11 @@ static int ensure_ws(sg_amp_plan *p, int B, int t_max) {
             // [2 kernels][items][8] shader-clock stamps, then [2 kernels][items][2] realtime start / end
             SG_ALLOC(p->tprof, p->tprof_items * 20 * sizeof(uint64_t));
             SG_HIP(hipMemset(p->tprof, 0, p->tprof_items * 20 * sizeof(uint64_t)));
+        }
+        if (p->cw2OT) {
+            SG_ALLOC(p->ws_c2xp, Bz * 2 * p->cw2OT * CW2_THREADS * 16);
+            SG_ALLOC(p->ws_c2vz, Bz * p->cw2OT * CW2_THREADS * 4);
+            SG_ALLOC(p->ws_c2part, Bz * 2 * p->Lblk * 16);
         }
         SG_ALLOC(p->ws_stM, Bz * p->L * rs);
         SG_ALLOC(p->ws_stI, Bz * p->L * rs);
@@ -459,6 +471,130 @@ static int build_cw(sg_amp_plan *p, const std::vector<int32_t> &row_k1, const st
     return SG_OK;
 }
 
+// Split per-codeword engine tables (amp_cw2.hip).  Output i at DCT position
+// K reads H[a] and H[b], b = N2 - a (fwd_coef), and its inverse input adds to
+// G[a] and G[b] (inv_contrib: first call a, second b): both touch only the
+// conjugate row pair {a mod P, P - a mod P} of the P-point stage.  Each output
+// is normalised so that a mod P is the smaller row of its pair (swapping a and
+// b takes (c1, c2) to (conj c2, conj c1) and (al, be) to (be, al):
+// Re(x) = Re(conj x)); the outputs of a pair go to one thread (the largest
+// pairs first, each to the least loaded thread), at most OT per thread; a
+// thread's slots list its pairs one after the other (CW_NEWROW on the first
+// output of a pair, CW_ENDROW on the last, CW_SELF when the pair's rows
+// coincide: r = 0 or P / 2).  Plus the first-FFT-stage masks of the
+// 16-values-per-thread transform (amp_cw2.hip c2_stage0_r32).
+static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::vector<int32_t> &row_k1,
+                     const std::vector<int32_t> &cls_ptr, const std::vector<uint32_t> &cls_ls) {
+    const long long N = p->w, N2 = p->N2;
+    const int P = p->rP, n = p->n, T = CW2_THREADS, Q = p->rQ;
+    if (P != 8192 || Q % 2 || p->Lblk > 2 * T || p->rmaxcls > 18 * T) return SG_OK;
+    struct Out { long long a; cd c1, c2, al, be; };
+    std::vector<Out> out(n);
+    std::vector<std::vector<int>> pair_of(P / 2 + 1);
+    for (int i = 0; i < n; ++i) {
+        Out &o = out[i];
+        long long b;
+        fwd_coef(o0[i], N, N2, sc, &o.a, &b, &o.c1, &o.c2);
+        int nc = 0;
+        bool ok = true;
+        o.al = o.be = cd(0, 0);
+        inv_contrib(o0[i], N, N2, sc, [&](long long k, cd c) {
+            if (nc++ == 0) {
+                ok = ok && k % N2 == o.a;
+                o.al = c;
+            } else {
+                ok = ok && k % N2 == b;
+                o.be = c;
+            }
+        });
+        SG_CHECK_ARG(ok && nc <= 2, "internal: inverse input of output %d outside its pair", i);
+        const int r = (int)(o.a % P), r2 = (P - r) % P;
+        if (r > r2) {  // normalise: a mod P is the smaller row of the pair
+            o.a = b;
+            const cd c1 = o.c1, al = o.al;
+            o.c1 = std::conj(o.c2);
+            o.c2 = std::conj(c1);
+            o.al = o.be;
+            o.be = al;
+        }
+        pair_of[(int)(o.a % P)].push_back(i);
+    }
+    std::vector<int> pairs;
+    for (int r = 0; r <= P / 2; ++r)
+        if (!pair_of[r].empty()) pairs.push_back(r);
+    std::stable_sort(pairs.begin(), pairs.end(),
+                     [&](int x, int y) { return pair_of[x].size() > pair_of[y].size(); });
+    std::vector<std::pair<int, int>> heap;  // (load, thread), min-heap
+    for (int i = 0; i < T; ++i) heap.push_back({0, i});
+    auto cmp = [](const std::pair<int, int> &x, const std::pair<int, int> &y) { return x > y; };
+    std::make_heap(heap.begin(), heap.end(), cmp);
+    std::vector<std::vector<int>> own(T);
+    int OT = 0;
+    for (int r : pairs) {
+        std::pop_heap(heap.begin(), heap.end(), cmp);
+        auto &h = heap.back();
+        own[h.second].push_back(r);
+        h.first += (int)pair_of[r].size();
+        OT = std::max(OT, h.first);
+        std::push_heap(heap.begin(), heap.end(), cmp);
+    }
+    if (OT > 16) return SG_OK;  // kernel instances for 12, 13, 14 and 16 outputs per thread
+    OT = OT <= 12 ? 12 : OT <= 14 ? OT : 16;
+    std::vector<uint32_t> ka((size_t)OT * T, 0u);
+    std::vector<int32_t> oi((size_t)OT * T, 0);
+    std::vector<float> cf((size_t)OT * T * 4, 0.f), gf((size_t)OT * T * 4, 0.f);
+    for (int tid = 0; tid < T; ++tid) {
+        int j = 0;
+        for (int r : own[tid]) {
+            const auto &lst = pair_of[r];
+            for (size_t q = 0; q < lst.size(); ++q, ++j) {
+                const int i = lst[q];
+                const Out &o = out[i];
+                uint32_t e = (uint32_t)o.a | CW_VALID;
+                if (q == 0) e |= CW_NEWROW;
+                if (q + 1 == lst.size()) e |= CW_ENDROW;
+                if (r == 0 || 2 * r == P) e |= CW_SELF;
+                const size_t c = (size_t)j * T + tid;
+                ka[c] = e;
+                oi[c] = i;
+                const float v[8] = {(float)o.c1.real(), (float)o.c1.imag(), (float)o.c2.real(), (float)o.c2.imag(),
+                                    (float)o.al.real(), (float)o.al.imag(), (float)o.be.real(), (float)o.be.imag()};
+                std::copy(v, v + 4, cf.begin() + 4 * c);
+                std::copy(v + 4, v + 8, gf.begin() + 4 * c);
+            }
+        }
+    }
+    // Which image values the class scatter (Ab, class m2 < Q) and the row
+    // writes (Az, entry Q) leave behind, as bits of the thread that reads
+    // them in the first FFT stage (c2_stage0_r32: complex index m1 = j + 256 g
+    // is value g & 15 of lane half g >> 4 of butterfly j; bit 2 (g & 15) + c)
+    std::vector<uint32_t> cmask((size_t)(Q + 1) * T, 0u);
+    auto mbit = [&](int m2, int m1, int c) {
+        const int j = m1 & 255, g = m1 >> 8;
+        const int tid = ((j >> 5) << 6) | ((g >> 4) << 5) | (j & 31);
+        cmask[(size_t)m2 * T + tid] |= 1u << (2 * (g & 15) + c);
+    };
+    for (int m2 = 0; m2 < Q; ++m2)
+        for (int q = cls_ptr[m2]; q < cls_ptr[m2 + 1]; ++q) {
+            const int loc = (int)(cls_ls[q] & 0xffffu);
+            mbit(m2, fsw(loc >> 1), loc & 1);  // fsw is its own inverse
+        }
+    for (int r : row_k1) {
+        mbit(Q, r, 0);
+        mbit(Q, r, 1);
+    }
+    SG_TRY(upload(p, &p->c2_cmask, cmask));
+    SG_TRY(upload(p, &p->c2_ka, ka));
+    SG_TRY(upload(p, &p->c2_oi, oi));
+    float *dcf = nullptr, *dgf = nullptr;
+    SG_TRY(upload(p, &dcf, cf));
+    SG_TRY(upload(p, &dgf, gf));
+    p->c2_cf = dcf;
+    p->c2_gf = dgf;
+    p->cw2OT = OT;
+    return SG_OK;
+}
+
 // Tables of the regular engine (amp_fused.hip), one transform per column
 // block: class order of each block's entries and the needed-row structure of
 // the two FFT stages.  Sizes: P = stage-1 FFT length (LDS resident), Q = N2/P.
@@ -690,7 +826,10 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
     SG_TRY(upload_cx(p, &p->r_twb, twb));
     if (p->precision == SG_F32 && nT == 1 && P == (1 << 13) && Lblk <= CW_THREADS && n <= 8 * CW_THREADS &&
         Q <= 64 && p->rmaxcls <= 9 * CW_THREADS && p->rimg == 2 * P && fpad(p->rmaxcls + 16) < p->rimg)
+    {
         SG_TRY(build_cw(p, row_k1[0], kptr[0], kk2[0], f_oa, f_ob, f_gi, f_gc, cls_ptr, cls_ls));
+        if (p->cw) SG_TRY(build_cw2(p, order0, t_scale[0], row_k1[0], cls_ptr, cls_ls));
+    }
     return SG_OK;
 }
 
@@ -729,6 +868,28 @@ static CwTables ctables(const sg_amp_plan *p) {
     tb.inv_n2 = 1.0f / (float)p->N2;
     tb.tprof = p->tprof;  // [B][32] stamps (the buffer holds B * Q * 20 >= 32 B words)
     return tb;
+}
+
+static Cw2Tables c2tables(const sg_amp_plan *p) {
+    Cw2Tables tb;
+    tb.L = p->L; tb.M = p->M; tb.LM = p->LM; tb.n = p->n; tb.N2 = p->N2; tb.Q = p->rQ; tb.Lblk = p->Lblk;
+    tb.OT = p->cw2OT; tb.maxcls = p->rmaxcls;
+    tb.inv_n2 = 1.0f / (float)p->N2;
+    tb.cmask = p->c2_cmask; tb.ka = p->c2_ka; tb.oi = p->c2_oi;
+    tb.cf = (const float4 *)p->c2_cf; tb.gf = (const float4 *)p->c2_gf;
+    tb.cls_ptr = p->r_cls_ptr; tb.cls_ls = p->r_cls_ls; tb.qpos = p->r_qpos; tb.seg = p->r_seg;
+    tb.xp = (float4 *)p->ws_c2xp; tb.vz = (float *)p->ws_c2vz; tb.part = (float4 *)p->ws_c2part;
+    tb.tprof = p->tprof;  // [2 B][64] stamps (the buffer holds B * Q * 20 >= 128 B words)
+    return tb;
+}
+
+// The split engine (amp_cw2.hip) runs the per-codeword engine's iterations
+// when its tables were built; SG_AMP_CW2=0 keeps the one-workgroup form
+// (A/B tests).
+static bool use_cw2(const sg_amp_plan *p) {
+    if (!p->cw2OT) return false;
+    const char *e = std::getenv("SG_AMP_CW2");
+    return !(e && std::strcmp(e, "0") == 0);
 }
 
 // Engine choice for a decode of B codewords: the per-codeword engine keeps
@@ -1146,7 +1307,10 @@ static int decode_regular(sg_amp_plan *p, const void *d_y, int B, const int32_t 
         handover = std::min(1.0, std::max(0.0, atof(h)));
     for (int t = 0; t < t_max - 1; ++t) {
         if constexpr (std::is_same<T, float>::value) {
-            if (cw) SG_TRY(cw_launch_iter(ctables(p), bf, sc, pr, t, s));
+            if (cw) {
+                if (use_cw2(p)) SG_TRY(cw2_launch_iter(c2tables(p), bf, sc, pr, t, s));
+                else SG_TRY(cw_launch_iter(ctables(p), bf, sc, pr, t, s));
+            }
         }
         if (!cw) {
             if (t > 0) SG_TRY(reg_launch_ab<T>(tb, bf, s));

@@ -242,7 +242,8 @@ int sg_profile_collect(double *total_ms, int64_t *launches) {
 
 const char *sg_phase_name(int phase) {
     static const char *names[SG_PH_COUNT] = {"ab_passA", "ab_passB", "az_passA", "az_passB", "eta",
-                                             "control", "bp_flood", "dense_gemm", "amp_iter"};
+                                             "control", "bp_flood", "dense_gemm", "amp_iter", "cw2_ab", "cw2_az",
+                                             "cw2_ctrl"};
     return (phase >= 0 && phase < SG_PH_COUNT) ? names[phase] : "unknown";
 }
 

@@ -47,8 +47,11 @@ def _amp_task(b):
     L, M = _S["L"], _S["M"]
     beta0 = np.zeros(L * M)
     beta0[np.arange(L) * M + _S["true"][b]] = 1.0
-    bh, tf, nmse, _ = sparc_ref.amp(_S["Y"][b], _S["W"], L, M, _S["n"], 1.0, _S["t_max"], _S["Ab"], _S["Az"], beta0)
-    return b, np.argmax(bh.reshape(L, M), 1).astype(np.int32), int(tf), np.asarray(nmse, np.float64)
+    psi = []
+    bh, tf, nmse, _ = sparc_ref.amp(_S["Y"][b], _S["W"], L, M, _S["n"], 1.0, _S["t_max"], _S["Ab"], _S["Az"], beta0,
+                                    trace=lambda t, d: psi.append(float(np.asarray(d["psi"]).ravel()[0])))
+    return (b, np.argmax(bh.reshape(L, M), 1).astype(np.int32), int(tf), np.asarray(nmse, np.float64),
+            np.asarray(psi, np.float64))
 
 
 def _init_bp(kind, ch, vdeg, cdeg, intrlv, max_it, factor):
@@ -112,13 +115,15 @@ def amp_pool(procs, W, L, M, n, o0, o1, Y, true, t_max):
 
 def amp_decode(procs, W, L, M, n, o0, o1, Y, true, t_max, deadline_s=1e9, order=None):
     """Decode the rows `order` (default: all) of Y with the CPU restatement on
-    `procs` processes.  Returns (dict b -> (map_idx, t_final, nmse), wall s)."""
+    `procs` processes.  Returns (dict b -> (map_idx, t_final, nmse, psi), wall s);
+    psi[t] is psi after iteration t + 1 (sparc.py:973-979), so the stop rule
+    compared psi[t] with psi[t - 1]."""
     pool = amp_pool(procs, W, L, M, n, o0, o1, Y, true, t_max)
     try:
         res, el = pool.run(_amp_task, list(order if order is not None else range(len(Y))), deadline_s)
     finally:
         pool.close()
-    return {b: (m, tf, nm) for b, m, tf, nm in res}, el
+    return {b: (m, tf, nm, ps) for b, m, tf, nm, ps in res}, el
 
 
 def bp_decode(procs, kind, ch, vdeg, cdeg, intrlv, max_it, factor, chunk=64, deadline_s=1e9):

@@ -1,0 +1,75 @@
+"""GPU parity of the split per-codeword engine (amp_cw2.hip) against the
+one-workgroup per-codeword engine (amp_cw.hip, SG_AMP_CW2=0) on the same
+plan, and against the CPU restatement of sparc.py:883-999 on the C2 size.
+
+Bars: NMSE after the first iterations within 2e-4 of the one-workgroup
+engine (the two differ only in f32 summation order); t_final within 1, or
+a threshold stop of an undecoded codeword (where one engine stopped, the
+other's relative psi change was within 10 % of rtol; at most 2 %);
+section decisions identical on >= 99.9 % of the sections; on the decodable
+R = 1.3 batch every codeword decodes identically.  The full-batch bar
+against the CPU restatement is test_amp_gpu.py::test_shipped_c2_batch_vs_oracle,
+which runs this engine (the automatic choice at B = 256)."""
+import numpy as np
+import pytest
+
+from ldpc_sparc_amd import _native, sparc
+
+pytestmark = pytest.mark.gpu
+
+
+def _batch(L, M, R, B, seed_design, seed_data, P=15.0):
+    n = int(round(L * np.log2(M) / R))
+    W = np.array(P)
+    o0, o1 = sparc.generate_ordering(W, n, L * M, seed_design)
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    rng = np.random.default_rng(seed_data)
+    true = rng.integers(0, M, (B, L)).astype(np.int32)
+    beta0 = np.zeros((B, L * M))
+    beta0[np.arange(B)[:, None], np.arange(L) * M + true] = 1
+    Y = op.apply(beta0, False) + rng.standard_normal((B, n))
+    return op, true, Y
+
+
+def _decode(monkeypatch, op, Y, true, cw2, t_max=25):
+    monkeypatch.setenv("SG_AMP_ENGINE", "cw")
+    monkeypatch.setenv("SG_AMP_CW2", "1" if cw2 else "0")
+    return sparc.amp_decode_batch(Y, op, 1.0, t_max, true_idx=true, precision=_native.SG_F32)
+
+
+@pytest.mark.parametrize("L,M,R,B", [(1024, 512, 1.5, 256), (1024, 512, 1.3, 256), (512, 512, 1.2, 256)])
+def test_split_engine_vs_one_workgroup_engine(monkeypatch, L, M, R, B):
+    op, true, Y = _batch(L, M, R, B, 41, 5)
+    ma, ta, na, pa = _decode(monkeypatch, op, Y, true, True)
+    mb, tb, nb, pb = _decode(monkeypatch, op, Y, true, False)
+    np.testing.assert_allclose(na[:, :4, 0], nb[:, :4, 0], atol=2e-4)
+    # t_final within 1, except threshold stops: where one engine stopped first,
+    # the other's relative psi change there was within 10 % of rtol = 1e-6
+    psi = {}
+
+    def rel_change(cw2, b, t):  # psi after iterations t - 1 and t (decodes with t_max = t, t + 1)
+        for tm in (t, t + 1):
+            if (cw2, tm) not in psi:
+                psi[cw2, tm] = _decode(monkeypatch, op, Y, true, cw2, tm)[3][:, 0]
+        return abs(psi[cw2, t + 1][b] - psi[cw2, t][b]) / abs(psi[cw2, t][b])
+
+    far = np.nonzero(np.abs(ta - tb) > 1)[0]
+    for b in far:
+        rc = rel_change(False, b, int(ta[b])) if ta[b] < tb[b] else rel_change(True, b, int(tb[b]))
+        assert rc <= 1.1e-6, (b, ta[b], tb[b], rc)
+        assert not (ma[b] == true[b]).all() and not (mb[b] == true[b]).all()  # undecoded on both sides
+    assert len(far) <= max(1, B // 50)
+    assert np.mean(ma == mb) >= 0.999
+    dec_b = (mb == true).all(1)
+    assert np.array_equal(ma[dec_b], mb[dec_b])  # codewords the one-workgroup engine decodes: identical
+    if R <= 1.3:
+        assert dec_b.mean() >= 0.75
+
+
+def test_split_engine_first_iterations_track(monkeypatch):
+    """psi after 1, 2, 3 iterations (t_max = 2, 3, 4) of the two engines."""
+    op, true, Y = _batch(1024, 512, 1.5, 256, 7, 9)
+    for tm in (2, 3, 4):
+        pa = _decode(monkeypatch, op, Y, true, True, tm)[3][:, 0]
+        pb = _decode(monkeypatch, op, Y, true, False, tm)[3][:, 0]
+        np.testing.assert_allclose(pa, pb, rtol=2e-6)

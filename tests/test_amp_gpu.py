@@ -523,41 +523,104 @@ def _c2_batch(seed_design, seed_data, B, R):
     return W, L, M, n, o0, o1, op, true, Y
 
 
-@pytest.mark.parametrize("R", [1.5, 1.3])
-def test_shipped_c2_batch_vs_oracle(monkeypatch, R):
+def _bench_c2_batch(R, seed=1, B=256):
+    """The received words bench.py times (bench.amp_setup: design seed 0,
+    Philox seed 1 stream 0, encode and AWGN on the GPU), downloaded."""
+    L, M, logM = 1024, 512, 9
+    n = int(round(L * logM / R))
+    W = np.array(15.0)
+    o0, o1 = sparc.generate_ordering(W, n, L * M, 0)
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    plan = op.plan(_native.SG_F32)
+    lib = _native.lib()
+    d_bits = _native.DeviceBuffer(B * L * logM)
+    d_true = _native.DeviceBuffer(B * L * 4)
+    d_x = _native.DeviceBuffer(B * n * 4)
+    d_y = _native.DeviceBuffer(B * n * 4)
+    _native.check(lib.sg_rng_bits_device(seed, 0, B, L * logM, d_bits.ptr, None))
+    _native.check(lib.sg_bits_to_sections_device(d_bits.ptr, B, L, logM, d_true.ptr, None))
+    _native.check(lib.sg_amp_encode_device(plan, d_true.ptr, B, d_x.ptr, None))
+    _native.check(lib.sg_awgn_device(_native.SG_F32, seed, 0, d_x.ptr, B, n, 1.0, d_y.ptr, None))
+    _native.synchronize()
+    Y = d_y.download(np.zeros((B, n), np.float32)).astype(np.float64)
+    true = d_true.download(np.zeros((B, L), np.int32))
+    return W, L, M, n, o0, o1, op, true, Y
+
+
+def _rel_change(psi, t):
+    """|psi_t - psi_(t-1)| / |psi_(t-1)| at iteration t >= 2 (psi[k] = psi after
+    iteration k + 1): what the stop rule of sparc.py:984-986 compares with rtol."""
+    return abs(psi[t - 1] - psi[t - 2]) / abs(psi[t - 2])
+
+
+@pytest.mark.parametrize("R,inputs", [(1.5, "host"), (1.3, "host"), (1.5, "bench"), (1.3, "bench")])
+def test_shipped_c2_batch_vs_oracle(monkeypatch, R, inputs):
     """The path bench.py times: C2 (L=1024, M=512, n=6144 at R=1.5 / 7089 at
     R=1.3), B=256, the automatic engine choice (per-codeword engine, hand-over
     to the staged engine once half the batch stopped), f32 -- against the CPU
-    restatement of sparc.py:883-999 (float128 softmax) on 16 codewords of the
-    batch.  f32 bar: t_final within 2 of the reference's; section
-    decisions identical on >= 99 % of the sections of every codeword (all of
-    them on codewords the reference decodes); NMSE per iteration within 1e-3
-    over the first 6 iterations."""
+    restatement of sparc.py:883-999 (float128 softmax) on ALL 256 codewords,
+    for a numpy-generated batch and for the bench's own Philox batch.
+
+    f32 bar ("AMP f32"):
+      * section decisions identical on >= 99 % of the sections of every
+        codeword, and on all of them where the reference decodes;
+      * t_final within 2 of the reference's, except for a threshold stop: the
+        engine that stopped first did so where the OTHER one's relative psi
+        change was within 10 % of rtol = 1e-6 (the stop rule compares a
+        change of ~1e-6 relative; psi itself agrees to ~2e-7, so near the
+        threshold f32 rounding decides the iteration; DESIGN.md traces the
+        bench batch's one such codeword); at most 1 % of the codewords;
+      * NMSE per iteration within 1e-3 over the first 6 iterations;
+      * FER identical, BER within 3 binomial standard deviations."""
     from oracle import cpu_pool
     monkeypatch.delenv("SG_AMP_ENGINE", raising=False)
     monkeypatch.delenv("SG_AMP_HANDOVER", raising=False)
-    B = 256
-    W, L, M, n, o0, o1, op, true, Y = _c2_batch(41, 7, B, R)
+    B, rtol = 256, 1e-6
+    if inputs == "host":
+        W, L, M, n, o0, o1, op, true, Y = _c2_batch(41, 7, B, R)
+    else:
+        W, L, M, n, o0, o1, op, true, Y = _bench_c2_batch(R)
     plan = op.plan(_native.SG_F32)
     assert _native.lib().sg_amp_plan_engine(plan, B) == 2
     mi, tf, nm, _ = sparc.amp_decode_batch(Y, op, 1.0, 25, true_idx=true, precision=_native.SG_F32)
     last = _native.amp_last_decode(plan)
     assert last["engine"] == 2
-    if R == 1.3:  # codewords stop after 14-18 iterations: the hand-over fires before the last ones stop
+    if R == 1.3 and inputs == "host":  # codewords stop after 14-18 iterations: the hand-over fires first
         assert 0 < last["handover_iter"] < int(tf.max()), (last, np.bincount(tf))
-    pick = list(range(0, B, B // 16))
-    res, _ = cpu_pool.amp_decode(cpu_pool.host_cores(8), W, L, M, n, o0, o1, Y, true, 25, order=pick)
-    assert sorted(res) == pick
-    for b in pick:
-        cm, ct_, cn = res[b]
-        assert abs(int(tf[b]) - ct_) <= 2, (b, tf[b], ct_)
+    res, _ = cpu_pool.amp_decode(cpu_pool.host_cores(16), W, L, M, n, o0, o1, Y, true, 25)
+    assert sorted(res) == list(range(B))
+    gpu_psi = {}
+
+    def gpu_rel_change(b, t):  # the GPU's psi after iterations t - 1 and t (decodes with t_max = t, t + 1)
+        for tm in (t, t + 1):
+            if tm not in gpu_psi:
+                gpu_psi[tm] = sparc.amp_decode_batch(Y, op, 1.0, tm, true_idx=true, precision=_native.SG_F32)[3][:, 0]
+        return abs(gpu_psi[t + 1][b] - gpu_psi[t][b]) / abs(gpu_psi[t][b])
+
+    threshold_stops = []
+    for b in range(B):
+        cm, ct_, cn, cpsi = res[b]
         same = np.mean(mi[b] == cm)
         if np.array_equal(cm, true[b]):
             assert same == 1.0, (b, same)
         assert same >= 0.99, (b, same)
         np.testing.assert_allclose(nm[b, :6, 0], cn[:6], atol=1e-3)
+        if abs(int(tf[b]) - ct_) > 2:
+            if tf[b] < ct_:  # the GPU stopped first: the reference was at its threshold there
+                rc = _rel_change(cpsi, int(tf[b]))
+            else:
+                rc = gpu_rel_change(b, ct_)
+            assert rc <= 1.1 * rtol, (b, tf[b], ct_, rc)
+            threshold_stops.append(b)
+    assert len(threshold_stops) <= B // 100, threshold_stops
+    cmap = np.stack([res[b][0] for b in range(B)])
+    assert np.array_equal((cmap != true).any(1), (mi != true).any(1))  # frame errors identical
+    nb = B * L * 9
+    cb = np.unpackbits((cmap ^ true).astype(np.uint32).view(np.uint8)).sum() / nb
+    gb = np.unpackbits((mi ^ true).astype(np.uint32).view(np.uint8)).sum() / nb
+    assert abs(cb - gb) <= 3 * np.sqrt(max(cb, 1.0 / nb) * (1 - cb) / nb) + 1.0 / nb, (cb, gb)
     if R == 1.3:  # decodable rate: most codewords decode, on both sides
-        assert np.mean([np.array_equal(res[b][0], true[b]) for b in pick]) >= 0.75
+        assert np.mean([np.array_equal(res[b][0], true[b]) for b in range(B)]) >= 0.75
 
 
 @pytest.mark.gpu

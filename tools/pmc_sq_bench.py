@@ -3,7 +3,7 @@ waits, VALU and LDS issue as fractions of wave cycles, LDS bank-conflict
 cycles as a fraction of LDS-array cycles (SQ_LDS_BANK_CONFLICT /
 SQ_LDS_IDX_ACTIVE, MI355X_MICROARCH.md LDS section).
 
-usage: python tools/pmc_sq_bench.py pass1.csv pass2.csv out.json"""
+usage: python tools/pmc_sq_bench.py pass1.csv pass2.csv out.json [kernel-prefix ...]"""
 import collections
 import csv
 import json
@@ -24,7 +24,8 @@ a1, n1 = load(sys.argv[1])
 a2, _ = load(sys.argv[2])
 out = {}
 for k in sorted(a1):
-    if not (k.startswith("cw_iter") or k.startswith("bp_flood_kernel")):
+    prefixes = sys.argv[4:] or ["cw_iter", "cw2_", "bp_flood_kernel"]
+    if not any(k.startswith(pf) for pf in prefixes):
         continue
     c = dict(a1[k])
     c.update(a2.get(k, {}))
