@@ -197,6 +197,8 @@ size_t cw_lds_bytes(int img, int nslots);
 // j < OT, grouped by conjugate row pair {r, P - r} of the P-point stage (host
 // build_cw2).  See DESIGN.md "Split per-codeword engine".
 constexpr int CW2_THREADS = 512;
+constexpr int CW2_SLICE = 9216;     // class entries per workgroup pass (18 per thread)
+constexpr uint32_t CW2_TRASH = 18432;  // LDS float index of the trash slot (after the image and statistics)
 constexpr uint32_t CW_SELF = 1u << 23;  // the pair's two rows coincide (r = 0 or P / 2)
 struct Cw2Tables {
     int L, M, LM, n, N2, Q, Lblk, OT, maxcls;
@@ -208,6 +210,7 @@ struct Cw2Tables {
     const float4 *gf;         // [OT][512] (al, be): G[a] += al z/phi, G[N2 - a] += be z/phi
     const int32_t *cls_ptr;   // [Q+1]
     const uint32_t *cls_ls;   // [Mc] padded real LDS index | section << 16
+    const uint32_t *cls2;     // [Q][9216] cls_ls of each class padded to 9216 entries with CW2_TRASH
     const int32_t *qpos;      // [Mc]
     const uint16_t *seg;      // [Q][Lblk+1]
     float4 *xp;               // [B][2][OT][512] partial (H[a], conj H[b]) of each half

@@ -155,7 +155,25 @@ __device__ __forceinline__ void c2_fft(cx<float> *d, int tid, uint32_t msk) {
 // LDS: the P-point image (64 KB), then the previous beta's section max and
 // 1/sum (stM, stI: 8 KB), staged once per launch.
 constexpr size_t C2_IMG_BYTES = (size_t)C2_P * 8;
-constexpr size_t C2_LDS_BYTES = C2_IMG_BYTES + 2 * 1024 * 4;
+constexpr size_t C2_LDS_BYTES = C2_IMG_BYTES + 2 * 1024 * 4 + 16;  // + the trash slot (CW2_TRASH)
+static_assert(CW2_TRASH == (C2_IMG_BYTES + 2 * 1024 * 4) / 4, "trash slot after the staged statistics");
+
+// Raw buffer resources: loads and stores address by a per-lane byte offset
+// plus a scalar one (no 64-bit address arithmetic on the vector ALUs), and
+// the hardware range check (offset >= bytes) returns 0 for loads and drops
+// stores -- the class slices' ragged ends need no clamps or branches.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t c2_rsrc(const void *p, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, bytes > 0 ? bytes : 0, 0x00020000);
+}
+__device__ __forceinline__ float c2_ldf(__amdgpu_buffer_rsrc_t r, int vo, int so) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
+}
+__device__ __forceinline__ uint32_t c2_ldu(__amdgpu_buffer_rsrc_t r, int vo, int so) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0);
+}
+// workgroup-uniform values (class bounds) in scalar registers: a buffer
+// resource built from them stays scalar (no waterfall loop)
+__device__ __forceinline__ int c2_uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 constexpr int C2_SN = C2_NC * C2_SC;  // class entries per thread
 
 
@@ -183,21 +201,25 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
     for (int m2 = h * Qh; m2 < (h + 1) * Qh; ++m2) {
         const int tl = c2_opaque(tid);
         C2_TPC(0);
-        const int q0 = tb.cls_ptr[m2], q1 = tb.cls_ptr[m2 + 1];
+        const int q0 = c2_uni(tb.cls_ptr[m2]), q1 = c2_uni(tb.cls_ptr[m2 + 1]);
         float v[C2_SN];
         uint32_t e[C2_SN];
+        {  // every load of the class slice in one round trip; past the class's end s reads 0 and the
+           // padded table points at the trash slot (sparc.py:429-432 below writes there harmlessly)
+            const __amdgpu_buffer_rsrc_t rs = c2_rsrc(s + q0, 4 * (q1 - q0));
+            const __amdgpu_buffer_rsrc_t re = c2_rsrc(tb.cls2 + (size_t)m2 * CW2_SLICE, 4 * CW2_SLICE);
 #pragma unroll
-        for (int i = 0; i < C2_SN; ++i) {  // every load of the class slice in one round trip
-            const int q = min(q0 + tl + i * C2_T, q1 - 1);
-            v[i] = s[q];
-            e[i] = tb.cls_ls[q];
+            for (int i = 0; i < C2_SN; ++i) {
+                v[i] = c2_ldf(rs, 4 * tl + 4 * i * C2_T, 0);
+                e[i] = c2_ldu(re, 4 * tl, 4 * i * C2_T);
+            }
         }
 #pragma unroll
         for (int c = 0; c < C2_NC; ++c) {  // beta = eta(s), sparc.py:429-432, scattered into the image
 #pragma unroll
             for (int i = c * C2_SC; i < (c + 1) * C2_SC; ++i) {
                 const int sec = e[i] >> 16;
-                if (q0 + tl + i * C2_T < q1) dr[e[i] & 0xffffu] = __expf((v[i] - sM[sec]) * inv_tp) * sI[sec];
+                dr[e[i] & 0xffffu] = __expf((v[i] - sM[sec]) * inv_tp) * sI[sec];
             }
             C2_TPC(1 + c);
         }
@@ -210,8 +232,9 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
         // owned indices a reloaded per class (L1) rather than held across the transform
         {
             uint32_t ka[OT];
+            const __amdgpu_buffer_rsrc_t rk = c2_rsrc(tb.ka, 4 * OT * C2_T);
 #pragma unroll
-            for (int j = 0; j < OT; ++j) ka[j] = tb.ka[j * C2_T + c2_opaque(tl)];
+            for (int j = 0; j < OT; ++j) ka[j] = c2_ldu(rk, 4 * c2_opaque(tl), 4 * j * C2_T);
 #pragma unroll
             for (int j = 0; j < OT; ++j) {
                 const uint32_t a = ka[j] & CW_KMASK;
@@ -359,15 +382,18 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
         C2_TPC(32);
         const uint32_t rmk = tb.cmask[tb.Q * C2_T + tl];
         {  // rows r and P - r of each owned pair: sum of al v conj(W) / be v W over its outputs
-           // (v = z / phi, al, be and a reloaded per class from L1 / L2: held across the transform
-           // they would spill)
-            uint32_t ka[OT];
+           // (a, v = z / phi, al, be reloaded per class from L1 / L2: held across the transform, or
+           // loaded one class ahead, they spill)
             cx<float> g1[OT], g2[OT];
+            uint32_t ka[OT];
+            const __amdgpu_buffer_rsrc_t rg = c2_rsrc(tb.gf, 16 * OT * C2_T), rv = c2_rsrc(vz, 4 * OT * C2_T),
+                                         rk = c2_rsrc(tb.ka, 4 * OT * C2_T);
 #pragma unroll
             for (int j = 0; j < OT; ++j) {
-                ka[j] = tb.ka[j * C2_T + tl];
-                const float4 gc = tb.gf[j * C2_T + tl];
-                const float vv = vz[j * C2_T + tl];
+                ka[j] = c2_ldu(rk, 4 * tl, 4 * j * C2_T);
+                const float4 gc = __builtin_bit_cast(
+                    float4, __builtin_amdgcn_raw_buffer_load_b128(rg, 16 * tl, 16 * j * C2_T, 0));
+                const float vv = c2_ldf(rv, 4 * tl, 4 * j * C2_T);
                 g1[j] = {gc.x * vv, gc.y * vv};
                 g2[j] = {gc.z * vv, gc.w * vv};
             }
@@ -397,16 +423,18 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
         C2_TPC(34);
         c2_fft<true>(d, tl, rmk);
         C2_TPC(35);
-        const int q0 = tb.cls_ptr[m2], q1 = tb.cls_ptr[m2 + 1];
+        const int q0 = c2_uni(tb.cls_ptr[m2]), q1 = c2_uni(tb.cls_ptr[m2 + 1]);
         float snv[C2_SN];
+        const __amdgpu_buffer_rsrc_t rs = c2_rsrc(s + q0, 4 * (q1 - q0));  // past the class's end: reads 0,
+                                                                           // stores dropped
         {
             float v[C2_SN];
             uint32_t e[C2_SN];
+            const __amdgpu_buffer_rsrc_t re = c2_rsrc(tb.cls2 + (size_t)m2 * CW2_SLICE, 4 * CW2_SLICE);
 #pragma unroll
             for (int i = 0; i < C2_SN; ++i) {  // every load of the class slice in one round trip
-                const int q = min(q0 + tl + i * C2_T, q1 - 1);
-                e[i] = tb.cls_ls[q];
-                v[i] = s[q];  // (t = 0: unused)
+                e[i] = c2_ldu(re, 4 * tl, 4 * i * C2_T);
+                v[i] = c2_ldf(rs, 4 * tl + 4 * i * C2_T, 0);  // (t = 0: unused)
             }
 #pragma unroll
             for (int i = 0; i < C2_SN; ++i) {
@@ -425,58 +453,51 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
         }
         C2_TPC(36);
 #pragma unroll
-        for (int c = 0; c < C2_SN; ++c) {  // s to HBM straight from the registers (class order)
-            const int q = q0 + tl + c * C2_T;
-            if (q < q1) s[q] = snv[c];
-        }
+        for (int c = 0; c < C2_SN; ++c)  // s to HBM straight from the registers (class order)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, snv[c]), rs, 4 * tl + 4 * c * C2_T, 0, 0);
         C2_TPC(37);
         __syncthreads();
         C2_TPC(38);
 #pragma unroll
-        for (int c = 0; c < C2_SN; ++c) {  // s of the class in class order, skewed by fpad
-            const int q = q0 + tl + c * C2_T;
-            if (q < q1) dr[fpad(q - q0)] = snv[c];
-        }
+        for (int c = 0; c < C2_SN; ++c) dr[fpad(tl + c * C2_T)] = snv[c];  // s of the class in class order,
+                                                                           // skewed by fpad (past the end: unread)
         __syncthreads();
         C2_TPC(39);
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
-            // partial of the section over its segment: running maximum, sums
-            // without the (first) maximum, two online chains (even / odd entries)
-            const int a = sa[k], b = sb[k];
+            // partial of the section over its segment: the maximum and its first
+            // position, then the sums of e and e^2 over the other entries
+            // (e = exp((x - max) / tau)); two passes over the class copy with
+            // selects instead of the online rescaling (fewer vector instructions)
+            const int a = sa[k], n = sb[k] - sa[k];
             constexpr int RC = 16;
-            float m = -INFINITY, S1 = 0.f, S2 = 0.f, mo = -INFINITY, S1o = 0.f, S2o = 0.f;
-            auto step = [&](float &mm, float &T1, float &T2, float xi) {
-                const bool up = xi > mm;
-                const float dlt = up ? (mm - xi) : (xi - mm);
-                const float ex = __expf(dlt * inv_tau);
-                T1 = up ? (T1 + 1.f) * ex : T1 + ex;
-                T2 = up ? (T2 + 1.f) * (ex * ex) : T2 + ex * ex;
-                mm = up ? xi : mm;
-            };
-            for (int c = a; c < b; c += RC) {
+            float m = -INFINITY;
+            int am = -1;
+            for (int c = 0; c < n; c += RC) {
                 float x[RC];
 #pragma unroll
-                for (int i = 0; i < RC; ++i) x[i] = dr[fpad(c + i)];  // inside the LDS image; masked below
+                for (int i = 0; i < RC; ++i) x[i] = dr[fpad(a + c + i)];  // inside the LDS image; masked below
 #pragma unroll
-                for (int i = 0; i < RC; i += 2) {
-                    if (c + i < b) step(m, S1, S2, x[i]);
-                    if (c + i + 1 < b) step(mo, S1o, S2o, x[i + 1]);
+                for (int i = 0; i < RC; ++i) {
+                    const bool up = c + i < n && x[i] > m;
+                    m = up ? x[i] : m;
+                    am = up ? c + i : am;
                 }
             }
-            if (mo > -INFINITY) {
-                if (mo > m) {
-                    const float f = __expf((m - mo) * inv_tau);
-                    S1 = (S1 + 1.f) * f + S1o;
-                    S2 = (S2 + 1.f) * (f * f) + S2o;
-                    m = mo;
-                } else {
-                    const float f = __expf((mo - m) * inv_tau);
-                    S1 += (1.f + S1o) * f;
-                    S2 += (1.f + S2o) * (f * f);
+            float S1 = 0.f, S2 = 0.f;
+            for (int c = 0; c < n; c += RC) {
+                float x[RC];
+#pragma unroll
+                for (int i = 0; i < RC; ++i) x[i] = dr[fpad(a + c + i)];
+#pragma unroll
+                for (int i = 0; i < RC; ++i) {
+                    float ex = __expf((x[i] - m) * inv_tau);
+                    ex = (c + i < n && c + i != am) ? ex : 0.f;
+                    S1 += ex;
+                    S2 += ex * ex;
                 }
             }
-            if (m > -INFINITY) {
+            if (m > -INFINITY) {  // merge into the section's running statistics
                 if (m > Mr[k]) {
                     const float f = __expf((Mr[k] - m) * inv_tau);
                     R1[k] = (R1[k] + 1.f) * f + S1;

@@ -70,7 +70,7 @@ struct sg_amp_plan {
     uint32_t *c_kt = nullptr;
     // split per-codeword engine (amp_cw2.hip): outputs per thread (0 = not built) and its tables
     int cw2OT = 0;
-    uint32_t *c2_ka = nullptr, *c2_cmask = nullptr;
+    uint32_t *c2_ka = nullptr, *c2_cmask = nullptr, *c2_cls = nullptr;
     int32_t *c2_oi = nullptr;
     void *c2_cf = nullptr, *c2_gf = nullptr;
     void *ws_c2xp = nullptr, *ws_c2vz = nullptr, *ws_c2part = nullptr;
@@ -487,7 +487,7 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
                      const std::vector<int32_t> &cls_ptr, const std::vector<uint32_t> &cls_ls) {
     const long long N = p->w, N2 = p->N2;
     const int P = p->rP, n = p->n, T = CW2_THREADS, Q = p->rQ;
-    if (P != 8192 || Q % 2 || p->Lblk > 2 * T || p->rmaxcls > 18 * T) return SG_OK;
+    if (P != 8192 || Q % 2 || p->Lblk > 2 * T || p->rmaxcls > CW2_SLICE) return SG_OK;
     struct Out { long long a; cd c1, c2, al, be; };
     std::vector<Out> out(n);
     std::vector<std::vector<int>> pair_of(P / 2 + 1);
@@ -583,6 +583,12 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
         mbit(Q, r, 0);
         mbit(Q, r, 1);
     }
+    // class tables padded to CW2_SLICE entries per class, the padding pointing
+    // at the trash slot (section 0), so the kernels need no range checks
+    std::vector<uint32_t> cls2((size_t)Q * CW2_SLICE, CW2_TRASH);
+    for (int m2 = 0; m2 < Q; ++m2)
+        std::copy(cls_ls.begin() + cls_ptr[m2], cls_ls.begin() + cls_ptr[m2 + 1], cls2.begin() + (size_t)m2 * CW2_SLICE);
+    SG_TRY(upload(p, &p->c2_cls, cls2));
     SG_TRY(upload(p, &p->c2_cmask, cmask));
     SG_TRY(upload(p, &p->c2_ka, ka));
     SG_TRY(upload(p, &p->c2_oi, oi));
@@ -877,7 +883,7 @@ static Cw2Tables c2tables(const sg_amp_plan *p) {
     tb.inv_n2 = 1.0f / (float)p->N2;
     tb.cmask = p->c2_cmask; tb.ka = p->c2_ka; tb.oi = p->c2_oi;
     tb.cf = (const float4 *)p->c2_cf; tb.gf = (const float4 *)p->c2_gf;
-    tb.cls_ptr = p->r_cls_ptr; tb.cls_ls = p->r_cls_ls; tb.qpos = p->r_qpos; tb.seg = p->r_seg;
+    tb.cls_ptr = p->r_cls_ptr; tb.cls_ls = p->r_cls_ls; tb.cls2 = p->c2_cls; tb.qpos = p->r_qpos; tb.seg = p->r_seg;
     tb.xp = (float4 *)p->ws_c2xp; tb.vz = (float *)p->ws_c2vz; tb.part = (float4 *)p->ws_c2part;
     tb.tprof = p->tprof;  // [2 B][64] stamps (the buffer holds B * Q * 20 >= 128 B words)
     return tb;
