@@ -72,6 +72,9 @@ def parse():
     ap.add_argument("--no-concat", action="store_true")
     ap.add_argument("--no-sc", action="store_true")
     ap.add_argument("--no-r13", action="store_true", help="skip the decodable-rate (R=1.3) C2 companion line")
+    ap.add_argument("--no-f64", action="store_true", help="skip the double-precision C2 companion line")
+    ap.add_argument("--bp-ebn0-extra", type=float, nargs="*", default=[1.0, 1.5],
+                    help="further C3 operating points (SURVEY.md 8(d): Eb/N0 1.0, 1.5, 2.0 dB)")
     ap.add_argument("--sc-batch", type=int, default=256)
     ap.add_argument("--sc-steps", type=int, default=2)
     ap.add_argument("--no-sc-notebook", action="store_true",
@@ -248,17 +251,22 @@ class HostCounterComm:
         pass
 
 
-PMC_TRAFFIC_FILES = ("r02_pmc_traffic_bench.json", "r01_pmc_traffic_bench.json")
+PMC_TRAFFIC_FILES = ("r03_pmc_traffic_bench.json", "r02_pmc_traffic_bench.json", "r01_pmc_traffic_bench.json")
 
 
-def pmc_traffic(section, field):
+def pmc_traffic(section, field, kernel_prefix=None):
     """HBM bytes per unit from the committed PMC passes of tools/pmc_bench.sh
-    over this bench (profiles/r02_pmc_traffic_bench.json, else the round-1
-    file): (value, file) or (None, None)."""
+    over this bench (the newest profiles/rNN_pmc_traffic_bench.json that has
+    the section -- and, with kernel_prefix, was measured on that kernel, so an
+    older engine's traffic is never reported for a newer one): (value, file)
+    or (None, None)."""
     for name in PMC_TRAFFIC_FILES:
         try:
             with open(os.path.join(REPO, "profiles", name)) as f:
-                return json.load(f)[section][field], name
+                sec = json.load(f)[section]
+            if kernel_prefix and not str(sec.get("kernel", "")).startswith(kernel_prefix):
+                continue
+            return sec[field], name
         except (OSError, KeyError, ValueError):
             continue
     return None, None
@@ -331,6 +339,36 @@ def amp_decodable(args, d, comm, cpu_seconds, procs):
            "avg_iterations": float(tf.mean()), "section_errors": int(cnt[0]), "bit_errors": int(cnt[1]),
            "codeword_errors": int(cnt[2]),
            "ber": float(cnt[1]) / (d.world * st["B"] * st["L"] * st["logM"])}
+    if cpu_seconds > 0:
+        out["cpu_baseline"] = amp_cpu_baseline(st, a, cpu_seconds, procs)
+    return out
+
+
+def amp_f64(args, d, comm, cpu_seconds, procs, steps=2):
+    """C2 at the reference's precision: the same design and Philox batch in
+    double precision (the f64 engine: staged regular engine, amp_fused.hip;
+    the reference computes in float64 with a float128 softmax, sparc.py:429-432,
+    463), with its decisions compared codeword by codeword with the CPU
+    restatement on a bounded sample."""
+    a = argparse.Namespace(**{**vars(args), "precision": "f64"})
+    st = amp_setup(a, d.rank)
+    amp_step(st, a, comm)
+    _native.device_synchronize()
+    d.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        amp_step(st, a, comm)
+    _native.device_synchronize()
+    el = d.max(time.perf_counter() - t0)
+    cnt = st["d_cnt"].download(np.zeros(4, np.int64))
+    tf = st["d_tf"].download(np.zeros(st["B"], np.int32))
+    out = {"workload": f"C2 in double precision: L=1024, M=512, n={st['n']}, R={args.rate}, t_max={args.t_max}, "
+                       "same design and batch as the f32 line",
+           "value": d.world * st["B"] * steps / el, "unit": "codewords/s", "dtype": "f64",
+           "batch_per_gpu": st["B"], "steps": steps, "avg_iterations": float(tf.mean()),
+           "engine": {1: "staged (amp_fused.hip)", 0: "general (amp_dct.hip)"}.get(
+               _native.lib().sg_amp_plan_engine(st["plan"], st["B"]), "?"),
+           "section_errors": int(cnt[0]), "bit_errors": int(cnt[1]), "codeword_errors": int(cnt[2])}
     if cpu_seconds > 0:
         out["cpu_baseline"] = amp_cpu_baseline(st, a, cpu_seconds, procs)
     return out
@@ -495,6 +533,18 @@ def bp_variant(args, d, std, rate, z, dectype, prec, ebn0, B, steps, max_it=50, 
                                "identical_iteration_counts": float((cit[done] == its[done]).mean()),
                                "cpu_fer": float((ch_[:, :c.K] != X[done][:, :c.K]).any(1).mean()),
                                "gpu_fer": float((hard[done][:, :c.K] != X[done][:, :c.K]).any(1).mean())}
+        cok = (ch_[:, :c.K] == X[done][:, :c.K]).all(1)  # codewords the CPU restatement decodes
+        nb = int(done.sum()) * c.K
+        out["cpu_baseline"].update({
+            "identical_decisions_where_cpu_decodes": float((ch_[cok] == hard[done][cok]).all(1).mean())
+            if cok.any() else None,
+            "cpu_ber": float((ch_[:, :c.K] != X[done][:, :c.K]).sum()) / nb,
+            "gpu_ber": float((hard[done][:, :c.K] != X[done][:, :c.K]).sum()) / nb,
+            "note": ("the CPU restatement runs in float64; the f32 engine's hard decisions of codewords that do "
+                     "not converge within max_it can differ in single bits, so 'identical_codeword_decisions' "
+                     "falls below 1 at low Eb/N0 while FER and the decoded codewords agree; f32 min-sum is "
+                     "bit-exact against a float32 restatement in tests/test_bp_f32_exact_gpu.py"
+                     if prec == _native.SG_F32 else "f64 on both sides")})
     return out
 
 
@@ -635,6 +685,8 @@ def concat_bench(args, d):
     ph = prof.stop()
     cnt = pipe.counts()
     gemm_ms = ph.get("dense_gemm", (0.0, 0))[0]
+    concat_traffic, concat_tfile = pmc_traffic("concat", "hbm_bytes_per_gemm_launch")
+    concat_mfma, _ = pmc_traffic("concat", "mfma_busy_frac")
     flops = 4.0 * n * L * M * B * (2 * 25 - 1) / 2 * args.concat_steps  # 2 n LM B per product, 49 products
     ach = flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms else None
     user_bits = Lu * 9 + mults * pipe.c.K
@@ -645,8 +697,20 @@ def concat_bench(args, d):
             "ebn0_db": args.concat_ebn0, "awgn_var": var, "R_overall": R_overall,
             "ber": float(cnt[1]) / (cnt[0] * user_bits) if cnt[0] else None,
             "codeword_errors": int(cnt[2]), "codewords": int(cnt[0]),
+            "cpu_baseline": {"value": None, "unit": "codewords/s", "cores": 0, "kind": "port",
+                             "sample": "none: infeasible on the host at this size -- the reference's dense "
+                                       "path (sparc_new.py:885-912, 1284-1294) holds A as a float64 "
+                                       f"{n} x {L * M} matrix ({8.0 * n * L * M / 1e9:.1f} GB) and runs two "
+                                       f"{2.0 * n * L * M / 1e9:.1f}-GFLOP matrix-vector products per AMP "
+                                       "iteration per codeword; the pipeline's pieces are parity-tested against "
+                                       "the CPU restatement at small L (tests/test_dense_gpu.py, "
+                                       "tests/test_pipeline_gpu.py)"},
             "roofline": {"bound": "mfma", "achieved": ach, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
-                         "frac": ach / MFMA_F32_PEAK_TFS if ach else None, "traffic": None,
+                         "frac": ach / MFMA_F32_PEAK_TFS if ach else None,
+                         "traffic": concat_traffic,
+                         "traffic_unit": "HBM bytes per gemm_f32_mfma launch (PMC FETCH_SIZE x2 + WRITE_SIZE, "
+                                         f"profiles/{concat_tfile})" if concat_traffic else None,
+                         "mfma_busy": concat_mfma,
                          "kernel": "gemm_f32_mfma (A beta split-K NT + A^T z NN, v_mfma_f32_32x32x2_f32)",
                          "algorithmic_flops_per_batch_iteration": 4.0 * n * L * M * B,
                          "kernel_ms": {k: round(v[0], 3) for k, v in ph.items()},
@@ -729,13 +793,19 @@ def main():
     # the engine this batch ran on (2: per-codeword amp_cw.hip, 1: staged amp_fused.hip)
     engine = _native.lib().sg_amp_plan_engine(st["plan"], st["B"])
     last = _native.amp_last_decode(st["plan"])
-    engine_name = {1: "staged (amp_fused.hip)", 2: "per-codeword (amp_cw.hip)"}.get(engine, str(engine))
+    split = phases.get("cw2_az", (0.0, 0))[1] > 0
+    engine_name = {1: "staged (amp_fused.hip)",
+                   2: ("split per-codeword (amp_cw2.hip)" if split else "per-codeword (amp_cw.hip)")}.get(
+        engine, str(engine))
     # rocprofv3 --pmc passes of tools/pmc_bench.sh over this bench command
-    traffic, tfile = pmc_traffic("amp", "hbm_bytes_per_codeword_iteration") if engine == 2 else (None, None)
+    traffic, tfile = (pmc_traffic("amp", "hbm_bytes_per_codeword_iteration", "cw2_" if split else "cw_iter")
+                      if engine == 2 else (None, None))
     cw_it_per_launch = cw_it / launches if launches else None
     tflops = flops_per_cwit * cw_it / (amp_ms * 1e-3) / 1e12 if amp_ms > 0 else None
     gbs = bytes_per_cwit * cw_it / (amp_ms * 1e-3) / 1e9 if amp_ms > 0 else None
-    kernel = ("cw_iter (one launch per AMP iteration of the batch)" if engine == 2 else
+    kernel = (("one AMP iteration of the batch = cw2_ab + cw2_ctrl + cw2_az + cw2_merge (four launches, "
+               "amp_cw2.hip; 'launch' below = one iteration)") if (engine == 2 and split) else
+              "cw_iter (one launch per AMP iteration of the batch)" if engine == 2 else
               "one AMP iteration = " + "+".join(AMP_PHASES[:6]))
     out = {
         "metric": METRIC,
@@ -785,6 +855,8 @@ def main():
     cpu_on = d.rank == 0 and d.world == 1 and args.cpu_seconds > 0
     if not args.no_r13:
         out["amp_r13"] = amp_decodable(args, d, comm, 0.75 * args.cpu_seconds if cpu_on else 0, procs)
+    if not args.no_f64 and args.precision == "f32":
+        out["amp_f64"] = amp_f64(args, d, comm, 0.25 * args.cpu_seconds if cpu_on else 0, procs)
 
     if not args.no_bp:
         bst = bp_setup(args, d.rank)
@@ -835,6 +907,12 @@ def main():
                                                       f"profiles/{bp_tfile})",
                                       "note": "SURVEY.md 8(d)'s figure assumes the messages stream through HBM; "
                                               "here they stay in LDS, so this bound does not bind (no frac)"}}
+
+    if not args.no_bp and args.bp_ebn0_extra:
+        # C3 at the survey's other operating points (1.0, 1.5, 2.0 dB), decisions vs the CPU
+        cs = 0.1 * args.cpu_seconds if cpu_on else 0.0
+        out["bp_ebn0"] = [bp_variant(args, d, "802.11n", "1/2", 81, "minsum", _native.SG_F32, e, args.bp_batch,
+                                     args.bp_steps, 50, cs, procs) for e in args.bp_ebn0_extra]
 
     if not args.no_bp:
         cs = 0.1 * args.cpu_seconds if cpu_on else 0.0

@@ -4,7 +4,9 @@ FETCH_SIZE (KB) x2 on gfx950 (wide coalesced reads tally half), WRITE_SIZE
 (KB) as is.  Bytes per dispatch, and per unit of work for the kernels whose
 unit the bench line states (C3 codeword-iterations, C4 codeword-iterations).
 
-usage: python tools/pmc_bench.py FETCH.csv WRITE.csv bench.json out.json"""
+usage: python tools/pmc_bench.py FETCH.csv WRITE.csv bench.json out.json
+(C5: the gemm_f32_mfma dispatches give the "concat" section's bytes per launch;
+tools/pmc_concat.sh adds its MFMA-busy fraction)"""
 import collections
 import csv
 import json
@@ -34,8 +36,24 @@ for k in sorted(set(fetch) | set(write)):
               "write_bytes_per_dispatch": write.get(k, 0.0) * 1024 / d}
 out = {"kernels": per, "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes; FETCH x2 (gfx950)"}
 rf = bench.get("roofline", {})
+c2k = [n for n in per if n.startswith("cw2_")]
 cwk = next((n for n in per if n.startswith("cw_iter")), None)
-if cwk and rf.get("codeword_iterations_per_launch"):
+if c2k and rf.get("codeword_iterations_per_launch"):
+    # split engine: every cw2_* dispatch of the decodes over the codeword-iterations they ran
+    # (cw2_az runs once per iteration of the batch)
+    tot = sum((per[k]["read_bytes_per_dispatch"] + per[k]["write_bytes_per_dispatch"]) * per[k]["dispatches"]
+              for k in c2k)
+    naz = sum(per[k]["dispatches"] for k in c2k if k.startswith("cw2_az"))
+    cwit = rf["codeword_iterations_per_launch"] * naz
+    out["amp"] = {"kernel": "+".join(sorted(c2k)), "hbm_bytes_per_iteration_launch_group": tot / max(naz, 1),
+                  "hbm_bytes_per_codeword_iteration": tot / cwit,
+                  "codeword_iterations_per_launch": rf["codeword_iterations_per_launch"],
+                  "per_kernel_bytes_per_codeword_iteration": {
+                      k: (per[k]["read_bytes_per_dispatch"] + per[k]["write_bytes_per_dispatch"]) * per[k][
+                          "dispatches"] / cwit for k in c2k},
+                  "algorithmic_bytes_per_codeword_iteration": bench.get("roofline_hbm", {}).get(
+                      "algorithmic_bytes_per_codeword_iteration")}
+elif cwk and rf.get("codeword_iterations_per_launch"):
     b = per[cwk]["read_bytes_per_dispatch"] + per[cwk]["write_bytes_per_dispatch"]
     out["amp"] = {"kernel": cwk, "hbm_bytes_per_launch": b,
                   "hbm_bytes_per_codeword_iteration": b / rf["codeword_iterations_per_launch"],
