@@ -282,7 +282,9 @@ def amp_setup(args, rank, rate=None):
     prec = _native.SG_F32 if args.precision == "f32" else _native.SG_F64
     o0, o1 = sparc.generate_ordering(W, n, L * M, 0)  # one design shared by every rank
     op = sparc.DesignOperator(W, L, M, n, o0, o1)
-    plan = op.plan(prec)
+    tp = time.perf_counter()
+    plan = op.plan(prec)  # host tables of every engine for this design (one-time, outside the timed region)
+    plan_s = time.perf_counter() - tp
     B = args.batch
     # throughput-mode input: Philox bits keyed by the rank
     # -> section indices -> x = A beta0 (sparc.py:51) -> AWGN, all on the GPU
@@ -300,7 +302,7 @@ def amp_setup(args, rank, rate=None):
     del d_bits, d_x
     st = dict(L=L, M=M, logM=logM, n=n, B=B, op=op, plan=plan, prec=prec, d_y=d_y, d_true=d_true,
               d_map=_native.DeviceBuffer(B * L * 4), d_tf=_native.DeviceBuffer(B * 4),
-              d_cnt=_native.DeviceBuffer(4 * 8), W=W, o0=o0, o1=o1)
+              d_cnt=_native.DeviceBuffer(4 * 8), W=W, o0=o0, o1=o1, plan_s=plan_s)
     return st
 
 
@@ -828,7 +830,8 @@ def main():
                                   "RCCL all-reduce of error counters)",
                    "counter_allreduce": counter_path, "rccl_ranks": rccl_ranks,
                    "engine_env": {}, "engine": engine_name,
-                   "handover_iter": last["handover_iter"]},
+                   "handover_iter": last["handover_iter"],
+                   "plan_build_s": round(st["plan_s"], 3)},
         "roofline": {"bound": "valu-f32", "achieved": tflops, "peak": VALU_PEAK_TFS, "unit": "TFLOP/s",
                      "frac": tflops / VALU_PEAK_TFS if tflops else None,
                      "traffic": traffic * cw_it_per_launch if (traffic and cw_it_per_launch) else None,

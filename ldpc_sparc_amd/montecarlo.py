@@ -318,7 +318,7 @@ class ConcatTrial:
 def concat_ber_sweep(L, M, n, P, L_unprotected, mults, ebn0_db, *, codewords, block=256, blocks_per_round=None,
                      rank=0, world=1, agg=None, design_seed=0, seed=0, t_max=25, bp_its=200, precision="f32",
                      ldpc=("802.11n", "1/2", 81), min_errors=None, checkpoint_dir=None, npz_file=None, rng="device",
-                     trial=None, max_rounds=None):
+                     trial=None, max_rounds=None, on_point=None):
     """BER / FER of concatenated SPARC + LDPC against Eb/N0 (the experiment of
     ldpc_sparc/performance_plots_general.py:100-138 for the plain concatenated
     decoder), `codewords` per point sharded over the ranks.  Eb/N0 to noise as
@@ -328,7 +328,8 @@ def concat_ber_sweep(L, M, n, P, L_unprotected, mults, ebn0_db, *, codewords, bl
     _min over the blocks rank 0 decoded, and snr_store = Eb/N0 in dB).
     `trial(point, first_block, n_blocks, block)` (counters as ConcatTrial's)
     replaces the GPU pipeline (CPU rehearsals: tools/c5_sweep.py --rehearsal); `max_rounds`
-    interrupts every point after that many rounds (run_point)."""
+    interrupts every point after that many rounds (run_point); `on_point(dict)`
+    is called with each point's result as soon as it is done."""
     from .ldpc import code
     agg = agg or Aggregator()
     logM = int(np.log2(M))
@@ -361,6 +362,8 @@ def concat_ber_sweep(L, M, n, P, L_unprotected, mults, ebn0_db, *, codewords, bl
                     "fer": float(tot[2]) / tot[0] if tot[0] else None,
                     "unprotected_bit_errors": int(tot[3]), "protected_bit_errors": int(tot[4]),
                     "R_overall": r_overall})
+        if on_point is not None:
+            on_point(out[-1])
     if npz_file and rank == 0:
         avg = np.array([[o["ber"] for o in out]], dtype=float)
         bb = [getattr(trial, "block_ber", {}).get(p, [np.nan]) for p in range(len(ebn0_db))]

@@ -100,11 +100,10 @@ def main():
                                       blocks_per_round=args.blocks_per_round, rank=rank, world=world,
                                       agg=agg, design_seed=args.design_seed, seed=args.seed,
                                       min_errors=args.min_errors, checkpoint_dir=args.checkpoint, npz_file=args.npz,
-                                      trial=trial, max_rounds=args.max_rounds)
+                                      trial=trial, max_rounds=args.max_rounds,
+                                      on_point=(lambda r: print(json.dumps(r), flush=True)) if rank == 0 else None)
     el = time.perf_counter() - t0
     if rank == 0:
-        for r in res:
-            print(json.dumps(r), flush=True)
         tot = sum(r["codewords"] for r in res)
         print(json.dumps({"codewords": tot, "seconds": el, "codewords_per_s": tot / el, "gpus": world,
                           "rehearsal": bool(args.rehearsal)}), flush=True)
