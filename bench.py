@@ -887,7 +887,8 @@ def main():
         lach = lds_bytes * cwit / (bp_ms * 1e-3) / 1e9 if bp_ms else None
         bbytes = 4 * (4 * c.Nmsg + c.N)
         bach = bbytes * cwit / (bp_ms * 1e-3) / 1e9 if bp_ms else None
-        hbm_meas, bp_tfile = pmc_traffic("bp", "hbm_bytes_per_codeword_iteration")
+        bp_kernel = c.decode_kernel("minsum", _native.SG_F32)
+        hbm_meas, bp_tfile = pmc_traffic("bp", "hbm_bytes_per_codeword_iteration", bp_kernel.split("<")[0])
         out["bp"] = {"workload": "C3: 802.11n r1/2 z=81 (n=1944), min-sum (corr 0.7), max 50 it, "
                                  f"Eb/N0 {args.bp_ebn0} dB, random codewords",
                      "value": d.world * bst["B"] * args.bp_steps / bel, "unit": "codewords/s",
@@ -896,13 +897,13 @@ def main():
                      "roofline": {"bound": "lds", "achieved": lach, "peak": lds_peak, "unit": "GB/s",
                                   "frac": lach / lds_peak if lach else None,
                                   "traffic": None,
-                                  "kernel": "bp_flood_kernel<float, minsum>",
+                                  "kernel": bp_kernel,
                                   "algorithmic_lds_bytes_per_codeword_iteration": lds_bytes,
                                   "kernel_ms": bp_ms, "launches": ph.get("bp_flood", (0, 0))[1],
                                   "note": "the messages never leave LDS: 16 Nmsg bytes of f32 message reads and "
                                           "writes per codeword-iteration against the LDS peak for that mix "
                                           "(ds_read_b32 128 B/clk/CU, ds_write_b32 64 B/clk/CU, harmonic mean, "
-                                          "2.4 GHz); SQ counters in profiles/r02_pmc_sq_bench.json"},
+                                          "2.4 GHz); SQ counters in profiles/r03_pmc_sq_bench.json"},
                      "roofline_hbm": {"bound": "hbm", "achieved_if_streamed": bach, "peak": HBM_PEAK_GBS,
                                       "unit": "GB/s", "algorithmic_bytes_per_codeword_iteration": bbytes,
                                       "traffic": hbm_meas,

@@ -152,6 +152,11 @@ int sg_ldpc_graph_create(const int64_t *vdeg, const int64_t *cdeg, const int64_t
 int sg_ldpc_graph_destroy(sg_graph *g);
 int sg_ldpc_graph_info(const sg_graph *g, int *nv, int *nc, int *nmsg, int *max_cdeg,
                        int *max_vdeg);
+/* Name of the kernel sg_ldpc_decode(_device) launches for this graph, decoder
+ * type and precision, as rocprofv3 lists it (e.g. "bp_grouped_minsum_kernel<4, 2>"
+ * for the degree-grouped single-precision min-sum kernel, "bp_flood_kernel<float,
+ * 1, 8, 4>" for the table kernel); NUL-terminated, truncated to len bytes. */
+int sg_ldpc_decode_kernel(const sg_graph *g, int dectype, int precision, char *name, size_t len);
 
 /* Batched flooding BP (replaces one c_ldpc.c sumprod/sumprod2/minsum call per
  * codeword, c_ldpc.c:32,138,339; driven serially by ldpc.py:463-490 and

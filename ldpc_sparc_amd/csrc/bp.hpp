@@ -24,6 +24,36 @@ struct BpArgs {
 
 template <typename T>
 int bp_launch(const BpArgs<T> &a, int dectype, int max_cdeg, hipStream_t s);
+
+// Degree-grouped layout of a Tanner graph (bp.hip "grouped min-sum kernel"):
+// variables and checks sorted by degree into groups of 64 (one wavefront
+// lane each) of equal degree, so every wave loop is uniform.  Check group g
+// of degree dc owns the dc x 64 message block at byte address addr_g
+// (slot = addr_g + 256 k + 4 lane); variable group g reads its ports' slot
+// byte addresses from the LDS table at tab_g + 128 k + 2 lane.  Groups are
+// assigned to the workgroup's 8 waves (at most GRP_VJ / GRP_CJ per wave).
+constexpr int GRP_WAVES = BP_THREADS / 64;
+constexpr int GRP_MAXDV = 16;  // variable degrees the unrolled variable groups take
+constexpr int GRP_MAXDC = 8;   // check degrees the unrolled check groups take
+struct BpGrpArgs {
+    const int32_t *meta;      // [5][GRP_WAVES][VJ or CJ]: vdeg, vtab, cdeg, caddr, cvalid (see bp.hip)
+    const int32_t *vmap;      // [GRP_WAVES][VJ][64] variable of each lane (-1: dummy)
+    const uint16_t *vtab;     // [ntab] slot byte addresses of the variable groups' ports
+    int ntab;                 // table entries
+    int msg_bytes;            // message image incl. the trash slot (16-byte multiple)
+    int vj, cj;               // groups per wave of the layout (<= the kernel's VJ, CJ)
+    int nv;
+    const float *ch;          // [B][nv]
+    float *app;               // [B][nv]
+    int32_t *it;              // [B]
+    int B, max_it;
+    float factor;
+};
+int bp_grouped_launch(const BpGrpArgs &a, hipStream_t s);
+// groups per wave of the kernel instance that takes a layout of vj / cj groups
+// per wave (the host lays meta / vmap out with these strides)
+inline int grp_kvj(int vj, int cj) { return (vj <= 4 && cj <= 2) ? 4 : 8; }
+inline int grp_kcj(int vj, int cj) { return (vj <= 4 && cj <= 2) ? 2 : 4; }
 template <typename T>
 int bp_count_launch(const T *app, const uint8_t *x, const int32_t *its, int B, int nv, int k,
                     int64_t *counts, hipStream_t s, int32_t *per_cw = nullptr);

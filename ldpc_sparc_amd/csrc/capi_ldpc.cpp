@@ -1,5 +1,8 @@
 // C ABI of the LDPC decoder: graph upload, batched decode, reference-compatible
 // scalar shims (ldpc.py:463-503 ctypes targets).
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -18,9 +21,146 @@ struct sg_graph {
     size_t cap_bytes = 0;
     int cap_b = 0;
     std::vector<int64_t> h_vdeg, h_cdeg, h_intrlv;  // kept for the shim cache
+    // degree-grouped layout for the single-precision min-sum kernel (bp.hpp)
+    bool grp_ok = false;
+    int grp_ntab = 0, grp_msg_bytes = 0, grp_vj = 0, grp_cj = 0;
+    int32_t *d_grp_meta = nullptr, *d_grp_vmap = nullptr;
+    uint16_t *d_grp_vtab = nullptr;
 };
 
 namespace sg {
+
+// Longest-processing-time assignment of groups (weights w) to GRP_WAVES waves
+// of at most `cap` groups each; returns the wave and position of every group.
+static void lpt_waves(const std::vector<int> &w, int cap, std::vector<int> &wave, std::vector<int> &pos) {
+    std::vector<int> order(w.size());
+    for (size_t i = 0; i < w.size(); ++i) order[i] = (int)i;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return w[x] > w[y]; });
+    std::vector<long> load(GRP_WAVES, 0);
+    std::vector<int> cnt(GRP_WAVES, 0);
+    wave.assign(w.size(), -1);
+    pos.assign(w.size(), -1);
+    for (int g : order) {
+        int best = -1;
+        for (int q = 0; q < GRP_WAVES; ++q)
+            if (cnt[q] < cap && (best < 0 || load[q] < load[best])) best = q;
+        wave[g] = best;
+        pos[g] = cnt[best]++;
+        load[best] += w[g];
+    }
+}
+
+// Degree-grouped layout (bp.hpp BpGrpArgs) of the graph, or false when the
+// graph does not fit the grouped kernel (degrees, group counts, 16-bit LDS
+// byte addresses).  voff/coff are the port offsets, intrlv the reference's
+// variable-port -> check-port map.
+static bool build_groups(sg_graph *g, const int64_t *vdeg, const int64_t *cdeg, const int64_t *intrlv,
+                         const std::vector<int32_t> &voff, const std::vector<int32_t> &coff, hipStream_t s) {
+    const int nv = g->nv, nc = g->nc;
+    if (g->max_cdeg > GRP_MAXDC || g->max_vdeg > GRP_MAXDV) return false;
+    // checks by degree (descending, stable), groups of 64 of one degree
+    std::vector<int> corder(nc);
+    for (int c = 0; c < nc; ++c) corder[c] = c;
+    std::stable_sort(corder.begin(), corder.end(), [&](int x, int y) { return cdeg[x] > cdeg[y]; });
+    std::vector<int> cg_deg, cg_first, cg_n;
+    for (int i = 0; i < nc;) {
+        const int d = (int)cdeg[corder[i]];
+        int n = 0;
+        while (i + n < nc && n < 64 && cdeg[corder[i + n]] == d) ++n;
+        cg_deg.push_back(d); cg_first.push_back(i); cg_n.push_back(n);
+        i += n;
+    }
+    std::vector<int> vorder(nv);
+    for (int v = 0; v < nv; ++v) vorder[v] = v;
+    std::stable_sort(vorder.begin(), vorder.end(), [&](int x, int y) { return vdeg[x] > vdeg[y]; });
+    std::vector<int> vg_deg, vg_first, vg_n;
+    for (int i = 0; i < nv;) {
+        const int d = (int)vdeg[vorder[i]];
+        int n = 0;
+        while (i + n < nv && n < 64 && vdeg[vorder[i + n]] == d) ++n;
+        vg_deg.push_back(d); vg_first.push_back(i); vg_n.push_back(n);
+        i += n;
+    }
+    const int ncg = (int)cg_deg.size(), nvg = (int)vg_deg.size();
+    const int cj = (ncg + GRP_WAVES - 1) / GRP_WAVES, vj = (nvg + GRP_WAVES - 1) / GRP_WAVES;
+    if (vj > 8 || cj > 4) return false;
+    const int KVJ = grp_kvj(vj, cj), KCJ = grp_kcj(vj, cj);
+    // check groups: weights = degree; message blocks laid out wave by wave
+    std::vector<int> cw, cp, vw, vp;
+    lpt_waves(cg_deg, cj, cw, cp);
+    std::vector<int> vweight(nvg);
+    for (int i = 0; i < nvg; ++i) vweight[i] = vg_deg[i] + 1;  // + the group's fixed cost
+    lpt_waves(vweight, vj, vw, vp);
+    std::vector<int32_t> meta(2 * GRP_WAVES * KVJ + 3 * GRP_WAVES * KCJ, 0);
+    int32_t *m_vdeg = meta.data(), *m_vtab = m_vdeg + GRP_WAVES * KVJ;
+    int32_t *m_cdeg = m_vtab + GRP_WAVES * KVJ, *m_caddr = m_cdeg + GRP_WAVES * KCJ, *m_cval = m_caddr + GRP_WAVES * KCJ;
+    std::vector<int32_t> caddr(ncg, 0);
+    long bytes = 0;
+    for (int w = 0; w < GRP_WAVES; ++w)
+        for (int q = 0; q < KCJ; ++q)
+            for (int i = 0; i < ncg; ++i)
+                if (cw[i] == w && cp[i] == q) {
+                    caddr[i] = (int32_t)bytes;
+                    bytes += 256L * cg_deg[i];
+                    m_cdeg[w * KCJ + q] = cg_deg[i];
+                    m_caddr[w * KCJ + q] = caddr[i];
+                    m_cval[w * KCJ + q] = cg_n[i];
+                }
+    const long trash = bytes;
+    const long msg_bytes = (bytes + 4 + 15) / 16 * 16;
+    if (msg_bytes > 65536) return false;
+    // check-port byte address of every message index (check c, port k)
+    std::vector<int32_t> cslot_base(nc);
+    for (int i = 0; i < ncg; ++i)
+        for (int l = 0; l < cg_n[i]; ++l) cslot_base[corder[cg_first[i] + l]] = caddr[i] + 4 * l;
+    std::vector<int32_t> msg_addr(g->nmsg);
+    for (int c = 0; c < nc; ++c)
+        for (int k = 0; k < coff[c + 1] - coff[c]; ++k) msg_addr[coff[c] + k] = cslot_base[c] + 256 * k;
+    // variable groups: table blocks [degree][64] wave by wave, lanes' variables
+    std::vector<int32_t> vmap((size_t)GRP_WAVES * KVJ * 64, -1);
+    std::vector<uint16_t> vtab;
+    for (int w = 0; w < GRP_WAVES; ++w)
+        for (int j = 0; j < KVJ; ++j)
+            for (int i = 0; i < nvg; ++i)
+                if (vw[i] == w && vp[i] == j) {
+                    const int d = vg_deg[i];
+                    m_vdeg[w * KVJ + j] = d;
+                    m_vtab[w * KVJ + j] = (int32_t)(2 * vtab.size());
+                    const size_t off = vtab.size();
+                    vtab.resize(off + 64 * (size_t)d, (uint16_t)trash);
+                    for (int l = 0; l < vg_n[i]; ++l) {
+                        const int v = vorder[vg_first[i] + l];
+                        vmap[(size_t)(w * KVJ + j) * 64 + l] = v;
+                        for (int k = 0; k < d; ++k) vtab[off + 64 * k + l] = (uint16_t)msg_addr[intrlv[voff[v] + k]];
+                    }
+                }
+    const size_t lds = (size_t)msg_bytes + (vtab.size() * 2 + 15) / 16 * 16;
+    if (lds > (size_t)BP_MAX_LDS || vtab.empty()) return false;
+    // every real port addresses a distinct 4-byte slot inside the message image
+    // and every check-group slot of a real check is reached exactly once
+    std::vector<uint8_t> hit(msg_bytes / 4, 0);
+    long real = 0;
+    for (uint16_t e : vtab) {
+        if (e == (uint16_t)trash) continue;
+        if (e % 4 || e >= trash || hit[e / 4]++) return false;
+        ++real;
+    }
+    if (real != g->nmsg) return false;
+    bool ok = hipMalloc(&g->d_grp_meta, sizeof(int32_t) * meta.size()) == hipSuccess &&
+              hipMalloc(&g->d_grp_vmap, sizeof(int32_t) * vmap.size()) == hipSuccess &&
+              hipMalloc(&g->d_grp_vtab, sizeof(uint16_t) * vtab.size()) == hipSuccess;
+    ok = ok && hipMemcpyAsync(g->d_grp_meta, meta.data(), sizeof(int32_t) * meta.size(), hipMemcpyHostToDevice, s) == hipSuccess &&
+         hipMemcpyAsync(g->d_grp_vmap, vmap.data(), sizeof(int32_t) * vmap.size(), hipMemcpyHostToDevice, s) == hipSuccess &&
+         hipMemcpyAsync(g->d_grp_vtab, vtab.data(), sizeof(uint16_t) * vtab.size(), hipMemcpyHostToDevice, s) == hipSuccess &&
+         hipStreamSynchronize(s) == hipSuccess;
+    if (!ok) return false;
+    g->grp_ntab = (int)vtab.size();
+    g->grp_msg_bytes = (int)msg_bytes;
+    g->grp_vj = vj;
+    g->grp_cj = cj;
+    g->grp_ok = true;
+    return true;
+}
 
 static int build_graph(const int64_t *vdeg, const int64_t *cdeg, const int64_t *intrlv, int nv, int nc,
                        int nmsg, sg_graph **out) {
@@ -77,6 +217,7 @@ static int build_graph(const int64_t *vdeg, const int64_t *cdeg, const int64_t *
         sg_ldpc_graph_destroy(g);
         return fail(SG_ERR_NOMEM, "device allocation/upload of the Tanner graph failed");
     }
+    build_groups(g, vdeg, cdeg, intrlv, voff, coff, s);  // (optional: the table kernel takes every graph)
     *out = g;
     return SG_OK;
 }
@@ -96,6 +237,12 @@ static BpArgs<T> make_args(sg_graph *g, const void *ch, int B, int max_it, doubl
     return a;
 }
 
+// SG_BP_GROUPED=0 routes single-precision min-sum to the table kernel (A/B)
+static bool use_grouped() {
+    const char *e = std::getenv("SG_BP_GROUPED");
+    return !(e && e[0] == '0');
+}
+
 static int decode_device(sg_graph *g, int dectype, int precision, const void *d_ch, int B, int max_it,
                          double corr, void *d_app, int32_t *d_it, hipStream_t s) {
     SG_CHECK_ARG(g, "graph is NULL");
@@ -111,6 +258,15 @@ static int decode_device(sg_graph *g, int dectype, int precision, const void *d_
         SG_HIP(hipMemcpyAsync(d_it, v.data(), sizeof(int32_t) * B, hipMemcpyHostToDevice, s));
         SG_HIP(hipStreamSynchronize(s));
         return SG_OK;
+    }
+    if (precision == SG_F32 && dectype == SG_MINSUM && g->grp_ok && use_grouped()) {
+        BpGrpArgs a;
+        a.meta = g->d_grp_meta; a.vmap = g->d_grp_vmap; a.vtab = g->d_grp_vtab;
+        a.ntab = g->grp_ntab; a.msg_bytes = g->grp_msg_bytes; a.vj = g->grp_vj; a.cj = g->grp_cj;
+        a.nv = g->nv;
+        a.ch = (const float *)d_ch; a.app = (float *)d_app; a.it = d_it;
+        a.B = B; a.max_it = max_it; a.factor = (float)corr;
+        return bp_grouped_launch(a, s);
     }
     if (precision == SG_F64)
         return bp_launch<double>(make_args<double>(g, d_ch, B, max_it, corr, d_app, d_it), dectype, g->max_cdeg, s);
@@ -224,6 +380,9 @@ int sg_ldpc_graph_destroy(sg_graph *g) {
     if (g->d_voff) hipFree(g->d_voff);
     if (g->d_port_slot) hipFree(g->d_port_slot);
     if (g->d_cdeg) hipFree(g->d_cdeg);
+    if (g->d_grp_meta) hipFree(g->d_grp_meta);
+    if (g->d_grp_vmap) hipFree(g->d_grp_vmap);
+    if (g->d_grp_vtab) hipFree(g->d_grp_vtab);
     if (g->d_ch) hipFree(g->d_ch);
     if (g->d_app) hipFree(g->d_app);
     if (g->d_it) hipFree(g->d_it);
@@ -238,6 +397,26 @@ int sg_ldpc_graph_info(const sg_graph *g, int *nv, int *nc, int *nmsg, int *max_
     if (nmsg) *nmsg = g->nmsg;
     if (max_cdeg) *max_cdeg = g->max_cdeg;
     if (max_vdeg) *max_vdeg = g->max_vdeg;
+    return SG_OK;
+}
+
+int sg_ldpc_decode_kernel(const sg_graph *g, int dectype, int precision, char *name, size_t len) {
+    using namespace sg;
+    SG_CHECK_ARG(g && name && len > 0, "null graph or name buffer");
+    SG_CHECK_ARG(dectype == SG_SUMPROD || dectype == SG_SUMPROD2 || dectype == SG_MINSUM,
+                 "Decoder type unknonwn (dectype=%d)", dectype);
+    SG_CHECK_ARG(precision == SG_F64 || precision == SG_F32, "precision must be SG_F64 or SG_F32");
+    char buf[96];
+    if (precision == SG_F32 && dectype == SG_MINSUM && g->grp_ok && use_grouped()) {
+        snprintf(buf, sizeof buf, "bp_grouped_minsum_kernel<%d, %d>", grp_kvj(g->grp_vj, g->grp_cj),
+                 grp_kcj(g->grp_vj, g->grp_cj));
+    } else {  // bp.hip dispatch_dc / dispatch_vj
+        const int dc = g->max_cdeg <= 8 ? 8 : g->max_cdeg <= 16 ? 16 : g->max_cdeg <= 24 ? 24 : 32;
+        const int vj = g->nv <= 4 * BP_THREADS ? 4 : BP_VJ;
+        snprintf(buf, sizeof buf, "bp_flood_kernel<%s, %d, %d, %d>", precision == SG_F64 ? "double" : "float",
+                 dectype, dc, vj);
+    }
+    snprintf(name, len, "%s", buf);
     return SG_OK;
 }
 

@@ -178,6 +178,15 @@ class code:
             self._graph = g
         return self._graph
 
+    def decode_kernel(self, dectype="minsum", precision=None):
+        """Name of the GPU kernel decode_batch launches for this code (as
+        rocprofv3 lists it): the degree-grouped min-sum kernel for
+        single-precision min-sum on graphs it takes, else the table kernel."""
+        prec = _native.SG_F32 if precision is None else precision
+        buf = ct.create_string_buffer(128)
+        _native.check(_native.lib().sg_ldpc_decode_kernel(self._device_graph(), _native.DECTYPES[dectype], prec, buf, 128))
+        return buf.value.decode()
+
     def __del__(self):
         g = getattr(self, "_graph", None)
         if g is not None and g.value:

@@ -64,7 +64,8 @@ bp = bench.get("bp")
 if bp:
     units = bp["batch_per_gpu"] * bp["avg_executed_iterations"]
     # the C3 line's kernel: f32 min-sum at check degree <= 8 (bp_variants add other instances)
-    k = next((n for n in per if n.replace(" ", "").startswith("bp_flood_kernel<float,2,8,")), None)
+    kn = str(bp["roofline"].get("kernel") or "bp_flood_kernel<float,2,8,").replace(" ", "")
+    k = next((n for n in per if n.replace(" ", "").startswith(kn)), None)
     if k:
         b = per[k]["read_bytes_per_dispatch"] + per[k]["write_bytes_per_dispatch"]
         out["bp"] = {"kernel": k, "hbm_bytes_per_codeword_iteration": b / units,

@@ -24,7 +24,7 @@ a1, n1 = load(sys.argv[1])
 a2, _ = load(sys.argv[2])
 out = {}
 for k in sorted(a1):
-    prefixes = sys.argv[4:] or ["cw_iter", "cw2_", "bp_flood_kernel"]
+    prefixes = sys.argv[4:] or ["cw_iter", "cw2_", "bp_flood_kernel", "bp_grouped"]
     if not any(k.startswith(pf) for pf in prefixes):
         continue
     c = dict(a1[k])
