@@ -413,183 +413,6 @@ int bp_launch(const BpArgs<T> &a, int dectype, int max_cdeg, hipStream_t s) {
 template int bp_launch<float>(const BpArgs<float> &, int, int, hipStream_t);
 template int bp_launch<double>(const BpArgs<double> &, int, int, hipStream_t);
 
-// ---------------------------------------------------------------- grouped min-sum kernel
-// Single-precision min-sum over the degree-grouped layout (bp.hpp BpGrpArgs,
-// built on the host by capi_ldpc.cpp build_groups).  The table kernel above is
-// bound by its vector-ALU issue (SQ: ~490 VALU and ~280 SALU instructions per
-// wave per iteration for the C3 code): per-lane degrees make every port loop
-// divergent, and the check update carries the argmin index and per-port sign
-// bits.  Here every group has one degree, so each wave runs straight-line code
-// unrolled for that degree, and the check update is
-//   m1 = min |L|, m2 = second min (m2 = min(m2, max(m1, |L|)), m1 = min(m1, |L|)),
-//   S = XOR of the raw words (its sign bit is the reference's `sall`),
-//   out_k = ((|L_k| == m1) ? m2 f : m1 f) with sign bit sign(L_k ^ S ^ f):
-// identical values to c_ldpc.c:339-381 -- the reference gives m2 only to its
-// first argmin, and a tied |L_k| == m1 elsewhere means m2 == m1; and
-// (neg ? -mag : mag) * f == +-(mag * f) exactly.  The variable pass keeps the
-// reference's port order (acc = ch + m_0 + m_1 + ..., c_ldpc.c:171-178).
-// Two LDS round trips per group and pass; 2 VALU per variable port, ~8 per
-// check port.
-template <int D>
-__device__ __forceinline__ float grp_var(unsigned char *lds, uint32_t tab, float acc) {
-    if constexpr (D == 0) {
-        return acc;
-    } else {
-        uint32_t sl[D];
-        float m[D];
-#pragma unroll
-        for (int k = 0; k < D; ++k) sl[k] = *reinterpret_cast<const uint16_t *>(lds + tab + 128 * k);
-#pragma unroll
-        for (int k = 0; k < D; ++k) m[k] = *reinterpret_cast<const float *>(lds + sl[k]);
-#pragma unroll
-        for (int k = 0; k < D; ++k) acc += m[k];
-#pragma unroll
-        for (int k = 0; k < D; ++k) *reinterpret_cast<float *>(lds + sl[k]) = acc - m[k];
-        return acc;
-    }
-}
-
-template <int DC>
-__device__ __forceinline__ uint32_t grp_check(unsigned char *lds, uint32_t addr, float factor, uint32_t fsign) {
-    float L[DC];
-#pragma unroll
-    for (int k = 0; k < DC; ++k) L[k] = *reinterpret_cast<const float *>(lds + addr + 256 * k);
-    float m1 = INFINITY, m2 = INFINITY;
-    uint32_t S = 0u;
-#pragma unroll
-    for (int k = 0; k < DC; ++k) {
-        const float a = fabsf(L[k]);
-        m2 = fminf(m2, fmaxf(a, m1));
-        m1 = fminf(m1, a);
-        S ^= __float_as_uint(L[k]);
-    }
-    const uint32_t unsat = (S >> 31) | (m1 > 0.0f ? 0u : 1u);
-    const float f1 = m1 * factor, f2 = m2 * factor;
-    const uint32_t Sf = S ^ fsign;
-#pragma unroll
-    for (int k = 0; k < DC; ++k) {
-        const float mag = fabsf(L[k]) == m1 ? f2 : f1;
-        *reinterpret_cast<float *>(lds + addr + 256 * k) =
-            __uint_as_float((__float_as_uint(mag) & 0x7fffffffu) | ((__float_as_uint(L[k]) ^ Sf) & 0x80000000u));
-    }
-    return unsat;
-}
-
-// uniform (per-wave) degree dispatch
-__device__ __forceinline__ float grp_var_d(int d, unsigned char *lds, uint32_t tab, float acc) {
-    switch (d) {
-#define SG_GV(N) case N: return grp_var<N>(lds, tab, acc);
-        SG_GV(0) SG_GV(1) SG_GV(2) SG_GV(3) SG_GV(4) SG_GV(5) SG_GV(6) SG_GV(7) SG_GV(8)
-        SG_GV(9) SG_GV(10) SG_GV(11) SG_GV(12) SG_GV(13) SG_GV(14) SG_GV(15) SG_GV(16)
-#undef SG_GV
-        default: return acc;  // (the host admits degrees <= GRP_MAXDV only)
-    }
-}
-__device__ __forceinline__ uint32_t grp_check_d(int d, unsigned char *lds, uint32_t addr, float f, uint32_t fs) {
-    switch (d) {
-#define SG_GC(N) case N: return grp_check<N>(lds, addr, f, fs);
-        SG_GC(2) SG_GC(3) SG_GC(4) SG_GC(5) SG_GC(6) SG_GC(7) SG_GC(8)
-#undef SG_GC
-        default: return 0u;
-    }
-}
-
-// meta layout: [0] vdeg[W][VJ], [1] vtab (byte address)[W][VJ],
-// [2] cdeg[W][CJ], [3] caddr (byte address)[W][CJ], [4] cvalid lanes[W][CJ]
-template <int VJ, int CJ>
-__global__ __launch_bounds__(BP_THREADS, 6) void bp_grouped_minsum_kernel(BpGrpArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    uint16_t *tabl = reinterpret_cast<uint16_t *>(smem + a.msg_bytes);
-    for (int i = tid; i < a.ntab; i += BP_THREADS) tabl[i] = a.vtab[i];
-    const int32_t *mv = a.meta + wave * VJ;
-    const int32_t *mc = a.meta + 2 * GRP_WAVES * VJ + wave * CJ;
-    // per-wave group parameters are uniform (scalar registers); the lanes'
-    // offsets are added at the use
-    int vd[VJ];
-    uint32_t vt[VJ];
-#pragma unroll
-    for (int j = 0; j < VJ; ++j) {
-        vd[j] = __builtin_amdgcn_readfirstlane(mv[j]);
-        vt[j] = (uint32_t)__builtin_amdgcn_readfirstlane(mv[GRP_WAVES * VJ + j] + a.msg_bytes);
-    }
-    int cdg[CJ], cn[CJ];
-    uint32_t ca[CJ];
-#pragma unroll
-    for (int q = 0; q < CJ; ++q) {
-        cdg[q] = __builtin_amdgcn_readfirstlane(mc[q]);
-        ca[q] = (uint32_t)__builtin_amdgcn_readfirstlane(mc[GRP_WAVES * CJ + q]);
-        cn[q] = __builtin_amdgcn_readfirstlane(mc[2 * GRP_WAVES * CJ + q]);
-    }
-    const int32_t *vmap = a.vmap + wave * VJ * 64 + lane;
-    const float factor = a.factor;
-    const uint32_t fsign = __float_as_uint(factor) & 0x80000000u;
-    const int nwords = a.msg_bytes / 4;
-    for (int cw = blockIdx.x; cw < a.B; cw += gridDim.x) {
-        const float *ch = a.ch + (size_t)cw * a.nv;
-        float chv[VJ], apv[VJ];
-#pragma unroll
-        for (int j = 0; j < VJ; ++j) {
-            const int v = j < a.vj ? vmap[64 * j] : -1;
-            chv[j] = v >= 0 ? ch[v] : 0.0f;
-            apv[j] = 0.0f;
-        }
-        for (int i = tid; i < nwords; i += BP_THREADS) reinterpret_cast<float *>(smem)[i] = 0.0f;
-        __syncthreads();
-        int it = 0;
-        for (; it < a.max_it; ++it) {
-#pragma unroll
-            for (int j = 0; j < VJ; ++j)
-                if (j < a.vj) apv[j] = grp_var_d(vd[j], smem, vt[j] + 2 * lane, chv[j]);
-            __syncthreads();
-            uint32_t unsat = 0u;
-#pragma unroll
-            for (int q = 0; q < CJ; ++q)
-                if (q < a.cj) {
-                    const uint32_t u = grp_check_d(cdg[q], smem, ca[q] + 4 * lane, factor, fsign);
-                    unsat |= lane < cn[q] ? u : 0u;
-                }
-            if (!__syncthreads_or((int)unsat)) break;  // c_ldpc.c:196-197
-        }
-        float *out = a.app + (size_t)cw * a.nv;
-#pragma unroll
-        for (int j = 0; j < VJ; ++j) {
-            const int v = j < a.vj ? vmap[64 * j] : -1;
-            if (v >= 0) out[v] = apv[j];
-        }
-        if (tid == 0) a.it[cw] = it;
-        __syncthreads();
-    }
-}
-
-template <int VJ, int CJ>
-static int grouped_one(const BpGrpArgs &a, hipStream_t s) {
-    auto kern = bp_grouped_minsum_kernel<VJ, CJ>;
-    const size_t lds = (size_t)a.msg_bytes + ((size_t)a.ntab * 2 + 15) / 16 * 16;
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BP_THREADS, lds) != hipSuccess || per_cu < 1)
-        per_cu = 1;
-    int grid = per_cu * device_cu_count();
-    if (grid > a.B) grid = a.B;
-    if (lds > 64 * 1024)
-        SG_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    ProfScope ps(SG_PH_BP, s);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(BP_THREADS), lds, s, a);
-    SG_HIP(hipGetLastError());
-    return SG_OK;
-}
-
-int bp_grouped_launch(const BpGrpArgs &a, hipStream_t s) {
-    const size_t lds = (size_t)a.msg_bytes + ((size_t)a.ntab * 2 + 15) / 16 * 16;
-    if (a.msg_bytes > 65536 || a.msg_bytes % 16 || lds > BP_MAX_LDS || a.vj < 1 || a.cj < 1 || a.vj > 8 || a.cj > 4)
-        return fail(SG_ERR_INVALID, "grouped BP layout out of range (msg %d B, table %d, %d/%d groups per wave)",
-                    a.msg_bytes, a.ntab, a.vj, a.cj);
-    if (a.B <= 0) return SG_OK;
-    if (grp_kvj(a.vj, a.cj) == 4) return grouped_one<4, 2>(a, s);
-    return grouped_one<8, 4>(a, s);
-}
-
 // ---------------------------------------------------------------- error counts
 // One workgroup per codeword: hard decision app < 0 (ldpc_awgn.py:97) against
 // the transmitted bits; counts over all nv bits (ldpc_awgn.py:99) and over the

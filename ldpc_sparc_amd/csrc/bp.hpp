@@ -35,6 +35,7 @@ int bp_launch(const BpArgs<T> &a, int dectype, int max_cdeg, hipStream_t s);
 constexpr int GRP_WAVES = BP_THREADS / 64;
 constexpr int GRP_MAXDV = 16;  // variable degrees the unrolled variable groups take
 constexpr int GRP_MAXDC = 8;   // check degrees the unrolled check groups take
+constexpr int GRP_FLAG_BYTES = 2 * GRP_WAVES * 4;  // LDS stop flags after the messages
 struct BpGrpArgs {
     const int32_t *meta;      // [5][GRP_WAVES][VJ or CJ]: vdeg, vtab, cdeg, caddr, cvalid (see bp.hip)
     const int32_t *vmap;      // [GRP_WAVES][VJ][64] variable of each lane (-1: dummy)

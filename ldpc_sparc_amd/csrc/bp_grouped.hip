@@ -1,0 +1,234 @@
+// Degree-grouped single-precision min-sum BP for gfx950 (the C3 path).
+//
+// Same decoder as bp.hip's table kernel for dectype SG_MINSUM / SG_F32
+// (c_ldpc.c:339-381 with the index fix of SURVEY.md 8(c); variable sums in the
+// reference's port order, c_ldpc.c:171-178), over the degree-grouped layout
+// of bp.hpp BpGrpArgs built by capi_ldpc.cpp build_groups.
+//
+// Why a second kernel: the table kernel is bound by vector-ALU issue (SQ: ~490
+// VALU and ~280 SALU instructions per wave per iteration on the C3 code, VALU
+// ~86 % busy): per-lane degrees make every port loop divergent, and its check
+// update carries the argmin index and per-port sign bits.  Here
+//   * every group has one degree, so each wave runs straight-line code
+//     unrolled for that degree (the per-wave degree is a scalar, dispatched
+//     by a scalar switch);
+//   * the check update is branch-free:
+//       m1 = min |L|, m2 = second min  (m2 = min(m2, max(m1, |L|)), m1 = min(m1, |L|)),
+//       S  = XOR of the raw words (its sign bit is the reference's `sall`),
+//       out_k = (|L_k| == m1 ? |m2 f| : |m1 f|) with sign bit of L_k ^ S ^ f,
+//     identical values to the reference: it gives m2 to its first argmin
+//     only, and a tie |L_k| == m1 elsewhere means m2 == m1; and
+//     (neg ? -mag : mag) * f == +-(mag * f) exactly;
+//   * the stopping test is a ballot per wave and one flag word per wave in
+//     LDS (double-buffered by iteration parity, so one barrier suffices), in
+//     place of __syncthreads_or (whose static LDS also offset every dynamic
+//     LDS address by 256 B, one add per port).
+// Per group and pass two LDS round trips; 2 VALU per variable port, ~7 per
+// check port.  Built with -fno-honor-nans: no NaN reaches the min/max (the
+// channel LLRs are finite and the messages are sums and products of them), so
+// the compiler drops the canonicalisation of their operands.
+#include "bp.hpp"
+
+namespace sg {
+
+// LDS words addressed by their byte address.  The kernel has no static LDS
+// (grouped_one checks), so its dynamic image starts at address 0 and the
+// table's slot addresses are used as they are: through the dynamic-LDS symbol
+// the compiler adds its (relocated, zero) base to every slot address, one VALU
+// per port.
+typedef __attribute__((address_space(3))) float lds_f32;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+__device__ __forceinline__ lds_f32 *ldsf(uint32_t byte) { return (lds_f32 *)(size_t)byte; }
+
+template <int D>
+__device__ __forceinline__ float grp_var(uint32_t tab, float acc) {
+    if constexpr (D == 0) {
+        return acc;
+    } else {
+        uint32_t sl[D];
+        float m[D];
+        const lds_u16 *t = (const lds_u16 *)(size_t)tab;
+#pragma unroll
+        for (int k = 0; k < D; ++k) sl[k] = t[64 * k];
+#pragma unroll
+        for (int k = 0; k < D; ++k) m[k] = *ldsf(sl[k]);
+#pragma unroll
+        for (int k = 0; k < D; ++k) acc += m[k];
+#pragma unroll
+        for (int k = 0; k < D; ++k) *ldsf(sl[k]) = acc - m[k];
+        return acc;
+    }
+}
+
+template <int DC>
+__device__ __forceinline__ uint32_t grp_check(uint32_t addr, float factor, uint32_t fsign) {
+    float L[DC];
+    lds_f32 *c = ldsf(addr);
+#pragma unroll
+    for (int k = 0; k < DC; ++k) L[k] = c[64 * k];
+    float m1 = INFINITY, m2 = INFINITY;
+    uint32_t S = 0u;
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        const float a = fabsf(L[k]);
+        m2 = fminf(m2, fmaxf(a, m1));
+        m1 = fminf(m1, a);
+        S ^= __float_as_uint(L[k]);
+    }
+    const uint32_t unsat = (S >> 31) | (m1 > 0.0f ? 0u : 1u);
+    // magnitudes of the two outputs, materialised once per check (kept out of
+    // the per-port select)
+    uint32_t b1 = __float_as_uint(m1 * factor) & 0x7fffffffu, b2 = __float_as_uint(m2 * factor) & 0x7fffffffu;
+    asm volatile("" : "+v"(b1), "+v"(b2));
+    const uint32_t Sf = S ^ fsign;
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        const uint32_t mag = fabsf(L[k]) == m1 ? b2 : b1;
+        c[64 * k] = __uint_as_float(((__float_as_uint(L[k]) ^ Sf) & 0x80000000u) | mag);
+    }
+    return unsat;
+}
+
+// uniform (per-wave) degree dispatch
+__device__ __forceinline__ float grp_var_d(int d, uint32_t tab, float acc) {
+    switch (d) {
+#define SG_GV(N) case N: return grp_var<N>(tab, acc);
+        SG_GV(0) SG_GV(1) SG_GV(2) SG_GV(3) SG_GV(4) SG_GV(5) SG_GV(6) SG_GV(7) SG_GV(8)
+        SG_GV(9) SG_GV(10) SG_GV(11) SG_GV(12) SG_GV(13) SG_GV(14) SG_GV(15) SG_GV(16)
+#undef SG_GV
+        default: return acc;  // (the host admits degrees <= GRP_MAXDV only)
+    }
+}
+__device__ __forceinline__ uint32_t grp_check_d(int d, uint32_t addr, float f, uint32_t fs) {
+    switch (d) {
+#define SG_GC(N) case N: return grp_check<N>(addr, f, fs);
+        SG_GC(2) SG_GC(3) SG_GC(4) SG_GC(5) SG_GC(6) SG_GC(7) SG_GC(8)
+#undef SG_GC
+        default: return 0u;
+    }
+}
+
+// LDS image: [msg_bytes) messages + trash slot, [2][GRP_WAVES] u32 stop flags
+// (GRP_FLAG_BYTES), then the variable groups' port table (u16 slot byte
+// addresses).
+
+// meta layout: [0] vdeg[W][VJ], [1] vtab (byte address)[W][VJ],
+// [2] cdeg[W][CJ], [3] caddr (byte address)[W][CJ], [4] cvalid lanes[W][CJ]
+template <int VJ, int CJ>
+__global__ __launch_bounds__(BP_THREADS, 6) void bp_grouped_minsum_kernel(BpGrpArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    uint32_t *flags = reinterpret_cast<uint32_t *>(smem + a.msg_bytes);
+    const uint32_t tab0 = a.msg_bytes + GRP_FLAG_BYTES;
+    uint16_t *tabl = reinterpret_cast<uint16_t *>(smem + tab0);
+    for (int i = tid; i < a.ntab; i += BP_THREADS) tabl[i] = a.vtab[i];
+    // per-wave group parameters are uniform (scalar registers); the lanes'
+    // offsets are added at the use
+    const int32_t *mv = a.meta + wave * VJ;
+    const int32_t *mc = a.meta + 2 * GRP_WAVES * VJ + wave * CJ;
+    int vd[VJ];
+    uint32_t vt[VJ];
+#pragma unroll
+    for (int j = 0; j < VJ; ++j) {
+        vd[j] = __builtin_amdgcn_readfirstlane(mv[j]);
+        vt[j] = (uint32_t)__builtin_amdgcn_readfirstlane(mv[GRP_WAVES * VJ + j]) + tab0;
+    }
+    int cdg[CJ], cn[CJ];
+    uint32_t ca[CJ];
+#pragma unroll
+    for (int q = 0; q < CJ; ++q) {
+        cdg[q] = __builtin_amdgcn_readfirstlane(mc[q]);
+        ca[q] = (uint32_t)__builtin_amdgcn_readfirstlane(mc[GRP_WAVES * CJ + q]);
+        cn[q] = __builtin_amdgcn_readfirstlane(mc[2 * GRP_WAVES * CJ + q]);
+    }
+    const int32_t *vmap = a.vmap + wave * VJ * 64 + lane;
+    const float factor = a.factor;
+    const uint32_t fsign = __float_as_uint(factor) & 0x80000000u;
+    const int nwords = a.msg_bytes / 4;
+    for (int cw = blockIdx.x; cw < a.B; cw += gridDim.x) {
+        const float *ch = a.ch + (size_t)cw * a.nv;
+        float chv[VJ], apv[VJ];
+#pragma unroll
+        for (int j = 0; j < VJ; ++j) {
+            const int v = j < a.vj ? vmap[64 * j] : -1;
+            chv[j] = v >= 0 ? ch[v] : 0.0f;
+            apv[j] = 0.0f;
+        }
+        for (int i = tid; i < nwords; i += BP_THREADS) reinterpret_cast<float *>(smem)[i] = 0.0f;
+        __syncthreads();
+        int it = 0;
+        for (; it < a.max_it; ++it) {
+            // ---- variable pass (c_ldpc.c:171-178)
+#pragma unroll
+            for (int j = 0; j < VJ; ++j)
+                if (j < a.vj) apv[j] = grp_var_d(vd[j], vt[j] + 2 * lane, chv[j]);
+            __syncthreads();
+            // ---- check pass (c_ldpc.c:183-194 with the min-sum update)
+            uint32_t unsat = 0u;
+#pragma unroll
+            for (int q = 0; q < CJ; ++q)
+                if (q < a.cj) {
+                    const uint32_t u = grp_check_d(cdg[q], ca[q] + 4 * lane, factor, fsign);
+                    unsat |= lane < cn[q] ? u : 0u;
+                }
+            // ---- stop when every check is satisfied (c_ldpc.c:196-197): one
+            // flag per wave, parity-buffered (this iteration's words were last
+            // read before the previous iteration's variable-pass barrier)
+            const uint32_t any = __ballot(unsat != 0u) != 0ull ? 1u : 0u;
+            uint32_t *fl = flags + (it & 1) * GRP_WAVES;
+            fl[wave] = any;
+            __syncthreads();
+            const uint4 f0 = *reinterpret_cast<const uint4 *>(fl);
+            const uint4 f1 = *reinterpret_cast<const uint4 *>(fl + 4);
+            if (((f0.x | f0.y | f0.z | f0.w) | (f1.x | f1.y | f1.z | f1.w)) == 0u) break;
+        }
+        float *out = a.app + (size_t)cw * a.nv;
+#pragma unroll
+        for (int j = 0; j < VJ; ++j) {
+            const int v = j < a.vj ? vmap[64 * j] : -1;
+            if (v >= 0) out[v] = apv[j];
+        }
+        if (tid == 0) a.it[cw] = it;
+        __syncthreads();
+    }
+}
+
+static size_t grouped_lds(const BpGrpArgs &a) {
+    return (size_t)a.msg_bytes + GRP_FLAG_BYTES + ((size_t)a.ntab * 2 + 15) / 16 * 16;
+}
+
+template <int VJ, int CJ>
+static int grouped_one(const BpGrpArgs &a, hipStream_t s) {
+    auto kern = bp_grouped_minsum_kernel<VJ, CJ>;
+    const size_t lds = grouped_lds(a);
+    static const size_t static_lds = [&] {
+        hipFuncAttributes fa;
+        return hipFuncGetAttributes(&fa, (const void *)kern) == hipSuccess ? (size_t)fa.sharedSizeBytes : (size_t)-1;
+    }();
+    if (static_lds != 0)  // the slot addresses assume the dynamic image at LDS address 0
+        return fail(SG_ERR_UNSUPPORTED, "grouped BP kernel has static LDS (%zu B)", static_lds);
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BP_THREADS, lds) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    int grid = per_cu * device_cu_count();
+    if (grid > a.B) grid = a.B;
+    if (lds > 64 * 1024)
+        SG_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    ProfScope ps(SG_PH_BP, s);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(BP_THREADS), lds, s, a);
+    SG_HIP(hipGetLastError());
+    return SG_OK;
+}
+
+int bp_grouped_launch(const BpGrpArgs &a, hipStream_t s) {
+    if (a.msg_bytes > 65536 || a.msg_bytes % 16 || grouped_lds(a) > BP_MAX_LDS || a.vj < 1 || a.cj < 1 ||
+        a.vj > 8 || a.cj > 4)
+        return fail(SG_ERR_INVALID, "grouped BP layout out of range (msg %d B, table %d, %d/%d groups per wave)",
+                    a.msg_bytes, a.ntab, a.vj, a.cj);
+    if (a.B <= 0) return SG_OK;
+    if (grp_kvj(a.vj, a.cj) == 4) return grouped_one<4, 2>(a, s);
+    return grouped_one<8, 4>(a, s);
+}
+
+}  // namespace sg

@@ -4,7 +4,7 @@
 set -e
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/abgrp; rm -rf $O; mkdir -p $O
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_bp_f32_exact_gpu.py tests/test_bp_gpu.py > $O/tests.log 2>&1
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_bp_grouped_gpu.py tests/test_bp_f32_exact_gpu.py tests/test_bp_gpu.py > $O/tests.log 2>&1
 A="--no-sc --no-sc-notebook --no-concat --no-r13 --no-f64 --cpu-seconds 0 --steps 1 --warmup 1 --bp-steps 10 --bp-ebn0-extra 1.0 1.5"
 for i in 1 2; do
   SG_BP_GROUPED=0 timeout -k 10 200 python bench.py $A > $O/old$i.json 2>$O/old$i.err
