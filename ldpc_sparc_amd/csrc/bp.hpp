@@ -28,18 +28,19 @@ int bp_launch(const BpArgs<T> &a, int dectype, int max_cdeg, hipStream_t s);
 // Degree-grouped layout of a Tanner graph (bp.hip "grouped min-sum kernel"):
 // variables and checks sorted by degree into groups of 64 (one wavefront
 // lane each) of equal degree, so every wave loop is uniform.  Check group g
-// of degree dc owns the dc x 64 message block at byte address addr_g
+// of degree dc owns the dc x 64 message block at LDS byte address addr_g
 // (slot = addr_g + 256 k + 4 lane); variable group g reads its ports' slot
-// byte addresses from the LDS table at tab_g + 128 k + 2 lane.  Groups are
-// assigned to the workgroup's 8 waves (at most GRP_VJ / GRP_CJ per wave).
+// byte addresses from the global table at entry tab_g / 2 + 64 k + lane.
+// Groups are assigned to the workgroup's 8 waves (at most 8 variable and 4
+// check groups per wave).
 constexpr int GRP_WAVES = BP_THREADS / 64;
 constexpr int GRP_MAXDV = 16;  // variable degrees the unrolled variable groups take
 constexpr int GRP_MAXDC = 8;   // check degrees the unrolled check groups take
-constexpr int GRP_FLAG_BYTES = 2 * GRP_WAVES * 4;  // LDS stop flags after the messages
+constexpr int GRP_FLAG_BYTES = 2 * GRP_WAVES * 4;  // LDS stop flags after the messages (the whole image)
 struct BpGrpArgs {
     const int32_t *meta;      // [5][GRP_WAVES][VJ or CJ]: vdeg, vtab, cdeg, caddr, cvalid (see bp.hip)
     const int32_t *vmap;      // [GRP_WAVES][VJ][64] variable of each lane (-1: dummy)
-    const uint16_t *vtab;     // [ntab] slot byte addresses of the variable groups' ports
+    const uint16_t *vtab;     // [ntab] LDS slot byte addresses of the variable groups' ports (global)
     int ntab;                 // table entries
     int msg_bytes;            // message image incl. the trash slot (16-byte multiple)
     int vj, cj;               // groups per wave of the layout (<= the kernel's VJ, CJ)

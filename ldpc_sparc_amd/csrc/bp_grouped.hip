@@ -13,7 +13,7 @@
 //     unrolled for that degree (the per-wave degree is a scalar, dispatched
 //     by a scalar switch);
 //   * the check update is branch-free:
-//       m1 = min |L|, m2 = second min  (m2 = min(m2, max(m1, |L|)), m1 = min(m1, |L|)),
+//       m1 = min |L|, m2 = second min  (m2 = med3(|L|, m1, m2), m1 = min(m1, |L|)),
 //       S  = XOR of the raw words (its sign bit is the reference's `sall`),
 //       out_k = (|L_k| == m1 ? |m2 f| : |m1 f|) with sign bit of L_k ^ S ^ f,
 //     identical values to the reference: it gives m2 to its first argmin
@@ -23,8 +23,8 @@
 //     LDS (double-buffered by iteration parity, so one barrier suffices), in
 //     place of __syncthreads_or (whose static LDS also offset every dynamic
 //     LDS address by 256 B, one add per port).
-// Per group and pass two LDS round trips; 2 VALU per variable port, ~7 per
-// check port.  Built with -fno-honor-nans: no NaN reaches the min/max (the
+// Per group and pass one table load (vector L1) and two LDS round trips;
+// 2 VALU per variable port, ~7 per check port.  Built with -fno-honor-nans: no NaN reaches the min/max (the
 // channel LLRs are finite and the messages are sums and products of them), so
 // the compiler drops the canonicalisation of their operands.
 #include "bp.hpp"
@@ -37,19 +37,21 @@ namespace sg {
 // the compiler adds its (relocated, zero) base to every slot address, one VALU
 // per port.
 typedef __attribute__((address_space(3))) float lds_f32;
-typedef __attribute__((address_space(3))) uint16_t lds_u16;
 __device__ __forceinline__ lds_f32 *ldsf(uint32_t byte) { return (lds_f32 *)(size_t)byte; }
 
+// Variable group of degree D: the lane's slot addresses straight from the
+// global port table (gtab = the lane's entry; the table is L1-resident and
+// shared by the CU's workgroups, so the LDS holds only the messages), then the
+// reference's sum in port order and the extrinsic write-backs.
 template <int D>
-__device__ __forceinline__ float grp_var(uint32_t tab, float acc) {
+__device__ __forceinline__ float grp_var(const uint16_t *gtab, float acc) {
     if constexpr (D == 0) {
         return acc;
     } else {
         uint32_t sl[D];
         float m[D];
-        const lds_u16 *t = (const lds_u16 *)(size_t)tab;
 #pragma unroll
-        for (int k = 0; k < D; ++k) sl[k] = t[64 * k];
+        for (int k = 0; k < D; ++k) sl[k] = gtab[64 * k];
 #pragma unroll
         for (int k = 0; k < D; ++k) m[k] = *ldsf(sl[k]);
 #pragma unroll
@@ -71,7 +73,7 @@ __device__ __forceinline__ uint32_t grp_check(uint32_t addr, float factor, uint3
 #pragma unroll
     for (int k = 0; k < DC; ++k) {
         const float a = fabsf(L[k]);
-        m2 = fminf(m2, fmaxf(a, m1));
+        m2 = __builtin_amdgcn_fmed3f(a, m1, m2);  // second smallest of {m1 <= m2, a}
         m1 = fminf(m1, a);
         S ^= __float_as_uint(L[k]);
     }
@@ -90,9 +92,9 @@ __device__ __forceinline__ uint32_t grp_check(uint32_t addr, float factor, uint3
 }
 
 // uniform (per-wave) degree dispatch
-__device__ __forceinline__ float grp_var_d(int d, uint32_t tab, float acc) {
+__device__ __forceinline__ float grp_var_d(int d, const uint16_t *gtab, float acc) {
     switch (d) {
-#define SG_GV(N) case N: return grp_var<N>(tab, acc);
+#define SG_GV(N) case N: return grp_var<N>(gtab, acc);
         SG_GV(0) SG_GV(1) SG_GV(2) SG_GV(3) SG_GV(4) SG_GV(5) SG_GV(6) SG_GV(7) SG_GV(8)
         SG_GV(9) SG_GV(10) SG_GV(11) SG_GV(12) SG_GV(13) SG_GV(14) SG_GV(15) SG_GV(16)
 #undef SG_GV
@@ -108,21 +110,21 @@ __device__ __forceinline__ uint32_t grp_check_d(int d, uint32_t addr, float f, u
     }
 }
 
-// LDS image: [msg_bytes) messages + trash slot, [2][GRP_WAVES] u32 stop flags
-// (GRP_FLAG_BYTES), then the variable groups' port table (u16 slot byte
-// addresses).
+// LDS image: [msg_bytes) messages + trash slot, then [2][GRP_WAVES] u32 stop
+// flags (GRP_FLAG_BYTES).
 
 // meta layout: [0] vdeg[W][VJ], [1] vtab (byte address)[W][VJ],
 // [2] cdeg[W][CJ], [3] caddr (byte address)[W][CJ], [4] cvalid lanes[W][CJ]
+// The LDS image is the messages and flags only (the port table is read from
+// global memory through L1; staging it in LDS measured 7 % slower: three
+// workgroups per CU instead of four), so four workgroups share a CU at
+// <4, 2> (8 waves per SIMD, <= 64 VGPRs); <8, 4> needs more registers.
 template <int VJ, int CJ>
-__global__ __launch_bounds__(BP_THREADS, 6) void bp_grouped_minsum_kernel(BpGrpArgs a) {
+__global__ __launch_bounds__(BP_THREADS, VJ <= 4 ? 8 : 6) void bp_grouped_minsum_kernel(BpGrpArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     uint32_t *flags = reinterpret_cast<uint32_t *>(smem + a.msg_bytes);
-    const uint32_t tab0 = a.msg_bytes + GRP_FLAG_BYTES;
-    uint16_t *tabl = reinterpret_cast<uint16_t *>(smem + tab0);
-    for (int i = tid; i < a.ntab; i += BP_THREADS) tabl[i] = a.vtab[i];
     // per-wave group parameters are uniform (scalar registers); the lanes'
     // offsets are added at the use
     const int32_t *mv = a.meta + wave * VJ;
@@ -132,7 +134,7 @@ __global__ __launch_bounds__(BP_THREADS, 6) void bp_grouped_minsum_kernel(BpGrpA
 #pragma unroll
     for (int j = 0; j < VJ; ++j) {
         vd[j] = __builtin_amdgcn_readfirstlane(mv[j]);
-        vt[j] = (uint32_t)__builtin_amdgcn_readfirstlane(mv[GRP_WAVES * VJ + j]) + tab0;
+        vt[j] = (uint32_t)__builtin_amdgcn_readfirstlane(mv[GRP_WAVES * VJ + j]) >> 1;  // table entry
     }
     int cdg[CJ], cn[CJ];
     uint32_t ca[CJ];
@@ -162,7 +164,7 @@ __global__ __launch_bounds__(BP_THREADS, 6) void bp_grouped_minsum_kernel(BpGrpA
             // ---- variable pass (c_ldpc.c:171-178)
 #pragma unroll
             for (int j = 0; j < VJ; ++j)
-                if (j < a.vj) apv[j] = grp_var_d(vd[j], vt[j] + 2 * lane, chv[j]);
+                if (j < a.vj) apv[j] = grp_var_d(vd[j], a.vtab + vt[j] + lane, chv[j]);
             __syncthreads();
             // ---- check pass (c_ldpc.c:183-194 with the min-sum update)
             uint32_t unsat = 0u;
@@ -194,9 +196,7 @@ __global__ __launch_bounds__(BP_THREADS, 6) void bp_grouped_minsum_kernel(BpGrpA
     }
 }
 
-static size_t grouped_lds(const BpGrpArgs &a) {
-    return (size_t)a.msg_bytes + GRP_FLAG_BYTES + ((size_t)a.ntab * 2 + 15) / 16 * 16;
-}
+static size_t grouped_lds(const BpGrpArgs &a) { return (size_t)a.msg_bytes + GRP_FLAG_BYTES; }
 
 template <int VJ, int CJ>
 static int grouped_one(const BpGrpArgs &a, hipStream_t s) {

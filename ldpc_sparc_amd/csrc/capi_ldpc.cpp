@@ -134,8 +134,7 @@ static bool build_groups(sg_graph *g, const int64_t *vdeg, const int64_t *cdeg, 
                         for (int k = 0; k < d; ++k) vtab[off + 64 * k + l] = (uint16_t)msg_addr[intrlv[voff[v] + k]];
                     }
                 }
-    const size_t lds = (size_t)msg_bytes + GRP_FLAG_BYTES + (vtab.size() * 2 + 15) / 16 * 16;
-    if (lds > (size_t)BP_MAX_LDS || vtab.empty()) return false;
+    if ((size_t)msg_bytes + GRP_FLAG_BYTES > (size_t)BP_MAX_LDS || vtab.empty()) return false;
     // every real port addresses a distinct 4-byte slot inside the message image
     // and every check-group slot of a real check is reached exactly once
     std::vector<uint8_t> hit(msg_bytes / 4, 0);
