@@ -198,7 +198,12 @@ size_t cw_lds_bytes(int img, int nslots);
 // build_cw2).  See DESIGN.md "Split per-codeword engine".
 constexpr int CW2_THREADS = 512;
 constexpr int CW2_SLICE = 9216;     // class entries per workgroup pass (18 per thread)
-constexpr uint32_t CW2_TRASH = 18432;  // LDS float index of the trash slot (after the image and statistics)
+// P-point image layout of the split engine: complex element i at c2pos(i) =
+// i + i / 32 (one pad value per 32), so every LDS access of the transform's
+// stages is a per-thread base plus a constant (amp_cw2.hip c2_fft)
+__host__ __device__ constexpr int c2pos(int i) { return i + (i >> 5); }
+constexpr uint32_t CW2_TRASH = 2 * (8192 + 256) + 2048;  // LDS float index of the trash slot (after the
+                                                         // padded image and the statistics)
 constexpr uint32_t CW_SELF = 1u << 23;  // the pair's two rows coincide (r = 0 or P / 2)
 struct Cw2Tables {
     int L, M, LM, n, N2, Q, Lblk, OT, maxcls;

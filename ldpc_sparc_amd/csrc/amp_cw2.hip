@@ -56,12 +56,80 @@ __device__ __forceinline__ cx<float> c2_w(const Cw2Tables &tb, uint32_t j) {
     return {__builtin_amdgcn_cosf(x), -__builtin_amdgcn_sinf(x)};
 }
 
+// ---- the P-point transform -------------------------------------------------
+// Complex values as two-float vectors, so the packed f32 instructions
+// (v_pk_add / v_pk_mul / v_pk_fma, with their operand swizzles and negations
+// as op_sel / neg modifiers) work on register pairs that stay paired: written
+// with a {x, y} struct, the compiler spent ~150 moves per transform re-pairing
+// them.  The image is addressed through LDS pointers built from complex
+// indices (the kernels have no static LDS, so the dynamic image starts at
+// address 0): every access of a stage is a per-thread base plus a constant,
+// folded into the instruction's offset.
+typedef float c2f __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) c2f c2lds;
+__device__ __forceinline__ c2lds *c2_at(int pos) { return (c2lds *)(size_t)(8u * (uint32_t)pos); }
+
+template <bool INV>
+__device__ __forceinline__ c2f c2_mi(c2f a) {  // * -i (forward), * +i (inverse)
+    return INV ? c2f{-a.y, a.x} : c2f{a.y, -a.x};
+}
+__device__ __forceinline__ c2f c2_mul(c2f a, c2f w) {  // two packed instructions
+    return __builtin_elementwise_fma(c2f{-a.y, a.y}, w.yx, a.xx * w);
+}
+
+template <bool INV>
+__device__ __forceinline__ void c2_dft4(c2f &a0, c2f &a1, c2f &a2, c2f &a3) {
+    const c2f t0 = a0 + a2, t1 = a0 - a2, t2 = a1 + a3, t3 = c2_mi<INV>(a1 - a3);
+    a0 = t0 + t2;
+    a2 = t0 - t2;
+    a1 = t1 + t3;
+    a3 = t1 - t3;
+}
+
+// 16-point DFT as 4 x 4 (fft.hpp dft16: inputs n = 4 n1 + n2, outputs k = k1 + 4 k2)
+template <bool INV>
+__device__ __forceinline__ void c2_dft16(c2f *a) {
+    const float c1 = 0.92387953251128675613f, s1 = 0.38268343236508977173f, r2 = 0.70710678118654752440f;
+    c2f y[4][4];
+#pragma unroll
+    for (int n2 = 0; n2 < 4; ++n2) {
+        c2f v0 = a[n2], v1 = a[n2 + 4], v2 = a[n2 + 8], v3 = a[n2 + 12];
+        c2_dft4<INV>(v0, v1, v2, v3);
+        y[n2][0] = v0;
+        y[n2][1] = v1;
+        y[n2][2] = v2;
+        y[n2][3] = v3;
+    }
+    // y[n2][k1] *= w16^(n2 k1): x (c - i s) forward, x (c + i s) inverse
+    auto tw = [&](c2f x, float c, float s) -> c2f {
+        return __builtin_elementwise_fma(INV ? c2f{-x.y, x.x} : c2f{x.y, -x.x}, c2f{s, s}, x * c2f{c, c});
+    };
+    y[1][1] = tw(y[1][1], c1, s1);
+    y[1][2] = tw(y[1][2], r2, r2);
+    y[1][3] = tw(y[1][3], s1, c1);
+    y[2][1] = tw(y[2][1], r2, r2);
+    y[2][2] = c2_mi<INV>(y[2][2]);
+    y[2][3] = tw(y[2][3], -r2, r2);
+    y[3][1] = tw(y[3][1], s1, c1);
+    y[3][2] = tw(y[3][2], -r2, r2);
+    y[3][3] = tw(y[3][3], -c1, -s1);
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) {
+        c2f v0 = y[0][k1], v1 = y[1][k1], v2 = y[2][k1], v3 = y[3][k1];
+        c2_dft4<INV>(v0, v1, v2, v3);
+        a[k1] = v0;
+        a[k1 + 4] = v1;
+        a[k1 + 8] = v2;
+        a[k1 + 12] = v3;
+    }
+}
+
 // lanes 32..63 of a <-> lanes 0..31 of b (v_permlane32_swap, no LDS)
-__device__ __forceinline__ void c2_swap32(cx<float> &a, cx<float> &b) {
+__device__ __forceinline__ void c2_swap32(c2f &a, c2f &b) {
     const auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.x), __float_as_uint(b.x), false, false);
     const auto ry = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.y), __float_as_uint(b.y), false, false);
-    a = {__uint_as_float(rx[0]), __uint_as_float(ry[0])};
-    b = {__uint_as_float(rx[1]), __uint_as_float(ry[1])};
+    a = c2f{__uint_as_float(rx[0]), __uint_as_float(ry[0])};
+    b = c2f{__uint_as_float(rx[1]), __uint_as_float(ry[1])};
 }
 
 // First Stockham stage at radix 32 (Ns = 1, no twiddles), 16 values per
@@ -75,22 +143,23 @@ __device__ __forceinline__ void c2_swap32(cx<float> &a, cx<float> &b) {
 // msk says whether component c of value jj was written for this transform
 // (host table, build_cw2), the stale ones read as zero.
 template <bool INV>
-__device__ __forceinline__ void c2_stage0_r32(cx<float> *d, int tid, uint32_t msk) {
-    const int l = tid & 63, H = l >> 5, j = ((tid >> 6) << 5) | (l & 31);
-    cx<float> v[16];
-    const int jp = fsw(j);  // adding multiples of 256 commutes with the swizzle
+__device__ __forceinline__ void c2_stage0_r32(int tid, uint32_t msk) {
+    const int l = tid & 63, H = l >> 5, w = tid >> 6, j = (w << 5) | (l & 31);
+    c2f v[16];
+    const c2lds *src = c2_at(j + w + 264 * 16 * H);  // c2pos(j + 256 m) = j + w + 264 m
 #pragma unroll
-    for (int jj = 0; jj < 16; ++jj) v[jj] = d[jp + ((16 * H + jj) << 8)];
+    for (int jj = 0; jj < 16; ++jj) v[jj] = src[264 * jj];
 #pragma unroll
     for (int jj = 0; jj < 16; ++jj) {  // all-ones / zero from the sign-extended bit
         const uint32_t mx = (uint32_t)((int)(msk << (31 - 2 * jj)) >> 31);
         const uint32_t my = (uint32_t)((int)(msk << (30 - 2 * jj)) >> 31);
-        v[jj] = {__uint_as_float(__float_as_uint(v[jj].x) & mx), __uint_as_float(__float_as_uint(v[jj].y) & my)};
+        v[jj] = c2f{__uint_as_float(__float_as_uint(v[jj].x) & mx), __uint_as_float(__float_as_uint(v[jj].y) & my)};
     }
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) c2_swap32(v[jj], v[jj + 8]);  // lane half H: x[J], x[16 + J], J = jj + 8 H
     {
-        // w32^jj = cos(2 pi jj / 32) -+ i sin(2 pi jj / 32), jj < 8 (forward -, inverse +)
+        // w32^J = cos(2 pi J / 32) -+ i sin(2 pi J / 32) for J = jj + 8 H (forward -, inverse +);
+        // w32^(jj + 8) = -i w32^jj
         constexpr float co[8] = {1.f, 0.98078528040323044913f, 0.92387953251128675613f, 0.83146961230254523708f,
                                  0.70710678118654752440f, 0.55557023301960222474f, 0.38268343236508977173f,
                                  0.19509032201612826785f};
@@ -99,43 +168,68 @@ __device__ __forceinline__ void c2_stage0_r32(cx<float> *d, int tid, uint32_t ms
                                  0.98078528040323044913f};
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) {
-            const cx<float> u = v[jj], x16 = v[jj + 8];
-            v[jj] = cadd(u, x16);
-            const cx<float> w = {co[jj], INV ? si[jj] : -si[jj]};
-            const cx<float> t = jj == 0 ? csub(u, x16) : cmul(csub(u, x16), w);  // (u - x16) w32^jj
-            v[jj + 8] = H ? mul_mi<float, INV>(t) : t;                              // * w32^(8 H)
+            const c2f u = v[jj], x16 = v[jj + 8];
+            v[jj] = u + x16;
+            const c2f wf = c2f{co[jj], INV ? si[jj] : -si[jj]};
+            const c2f w = H ? c2_mi<INV>(wf) : wf;
+            v[jj + 8] = c2_mul(u - x16, w);  // (jj = 0: w = 1 or -+i, exact)
         }
     }
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) c2_swap32(v[jj], v[jj + 8]);  // lane half p: sub-sequence p, J = 0..15
-    dft16<float, INV>(v);                                        // v[q] = X_j[2 q + H]
+    c2_dft16<INV>(v);                                            // v[q] = X_j[2 q + H]
     __syncthreads();
+    c2lds *dst = c2_at(33 * j + H);  // c2pos(32 j + 2 q + H) = 33 j + 2 q + H
 #pragma unroll
-    for (int q = 0; q < 16; ++q) d[fsw((j << 5) | (q << 1) | H)] = v[q];
+    for (int q = 0; q < 16; ++q) dst[2 * q] = v[q];
     __syncthreads();
 }
 
-// Radix-16 stage with Ns = 2^LNS (fft.hpp stockham1_stage_ct, one butterfly
-// per thread) and its stage twiddles w_(16 Ns)^(e k) from the hardware sine /
-// cosine (e = 1, 2, 3, 4, 8, 12; the others as products, fft.hpp tw_apply)
+// Radix-16 Stockham stage with Ns = 2^LNS (>= 32), one butterfly j = tid per
+// thread: inputs x[j + 512 r], twiddles w_(16 Ns)^(r k) (k = j mod Ns) from
+// two hardware sine / cosine pairs (w, w^4) and packed products (w^2, w^3,
+// w^8, w^12, then the 15 powers as in fft.hpp tw_apply), 16-point DFT,
+// outputs at b + Ns r, b = 16 (j - k) + k.
 template <bool INV, int LNS>
-__device__ __forceinline__ void c2_stage_r16(cx<float> *d, int tid) {
-    cx<float> wl[6];
-    constexpr float inv = 1.0f / (float)(1 << (LNS + 4));
-    const int k = tid & ((1 << LNS) - 1);
+__device__ __forceinline__ void c2_stage_r16(int tid) {
+    constexpr int NS = 1 << LNS;
+    static_assert(NS >= 32, "c2pos offsets assume Ns a multiple of 32");
+    const int j = tid, k = j & (NS - 1);
+    c2f v[16];
+    const c2lds *src = c2_at(j + (j >> 5));  // c2pos(j + 512 r) = c2pos(j) + 528 r
 #pragma unroll
-    for (int q = 0; q < 6; ++q) {
-        const float x = (float)((tw_exp(16, q) * k) & ((1 << (LNS + 4)) - 1)) * inv;
-        wl[q] = {__builtin_amdgcn_cosf(x), -__builtin_amdgcn_sinf(x)};
+    for (int r = 0; r < 16; ++r) v[r] = src[528 * r];
+    {
+        constexpr float inv = 1.0f / (float)(16 * NS);
+        const float x1 = (float)k * inv, x4 = (float)((4 * k) & (16 * NS - 1)) * inv;
+        const c2f w1 = c2f{__builtin_amdgcn_cosf(x1), INV ? __builtin_amdgcn_sinf(x1) : -__builtin_amdgcn_sinf(x1)};
+        const c2f w4 = c2f{__builtin_amdgcn_cosf(x4), INV ? __builtin_amdgcn_sinf(x4) : -__builtin_amdgcn_sinf(x4)};
+        const c2f w2 = c2_mul(w1, w1), w3 = c2_mul(w2, w1), w8 = c2_mul(w4, w4), w12 = c2_mul(w8, w4);
+        const c2f wb[3] = {w1, w2, w3}, wq[3] = {w4, w8, w12};
+#pragma unroll
+        for (int b = 1; b < 4; ++b) v[b] = c2_mul(v[b], wb[b - 1]);
+#pragma unroll
+        for (int q = 1; q < 4; ++q) {
+            v[4 * q] = c2_mul(v[4 * q], wq[q - 1]);
+#pragma unroll
+            for (int b = 1; b < 4; ++b) v[4 * q + b] = c2_mul(v[4 * q + b], c2_mul(wq[q - 1], wb[b - 1]));
+        }
     }
-    stockham1_stage_ct<float, INV, 16, C2_EPT, C2_LOG2P, LNS>(d, wl, tid);
+    c2_dft16<INV>(v);
+    const int bo = ((j - k) << 4) + k;
+    __syncthreads();
+    c2lds *dst = c2_at(bo + (bo >> 5));  // c2pos(bo + Ns r) = c2pos(bo) + (Ns + Ns / 32) r
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dst[(NS + NS / 32) * r] = v[r];
+    __syncthreads();
 }
 
+// Natural-order P-point DFT of the image (element i at c2pos(i)), in place
 template <bool INV>
-__device__ __forceinline__ void c2_fft(cx<float> *d, int tid, uint32_t msk) {
-    c2_stage0_r32<INV>(d, tid, msk);
-    c2_stage_r16<INV, 5>(d, c2_opaque(tid));
-    c2_stage_r16<INV, 9>(d, c2_opaque(tid));
+__device__ __forceinline__ void c2_fft(int tid, uint32_t msk) {
+    c2_stage0_r32<INV>(tid, msk);
+    c2_stage_r16<INV, 5>(c2_opaque(tid));
+    c2_stage_r16<INV, 9>(c2_opaque(tid));
 }
 
 }  // namespace
@@ -154,7 +248,7 @@ __device__ __forceinline__ void c2_fft(cx<float> *d, int tid, uint32_t msk) {
 // ---------------------------------------------------------------------------- Ab
 // LDS: the P-point image (64 KB), then the previous beta's section max and
 // 1/sum (stM, stI: 8 KB), staged once per launch.
-constexpr size_t C2_IMG_BYTES = (size_t)C2_P * 8;
+constexpr size_t C2_IMG_BYTES = (size_t)c2pos(C2_P) * 8;  // padded: element i at c2pos(i)
 constexpr size_t C2_LDS_BYTES = C2_IMG_BYTES + 2 * 1024 * 4 + 16;  // + the trash slot (CW2_TRASH)
 static_assert(CW2_TRASH == (C2_IMG_BYTES + 2 * 1024 * 4) / 4, "trash slot after the staged statistics");
 
@@ -180,7 +274,6 @@ constexpr int C2_SN = C2_NC * C2_SC;  // class entries per thread
 template <int OT>
 __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> bf) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    cx<float> *d = reinterpret_cast<cx<float> *>(smem);
     float *dr = reinterpret_cast<float *>(smem);
     float *sM = reinterpret_cast<float *>(smem + C2_IMG_BYTES), *sI = sM + 1024;
     const int h = blockIdx.x & 1, cw = blockIdx.x >> 1, tid = threadIdx.x;
@@ -191,7 +284,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
         sI[l] = bf.stI[lb + l];
     }
     const float inv_tp = (float)(1.0 / bf.tau[cw]);
-    const float *s = bf.s + (size_t)cw * tb.LM;
+    float *s = bf.s + (size_t)cw * tb.LM;  // s in; beta out (read by cw2_az, which writes the new s)
     cx<float> Ha[OT], Hb[OT];  // H[a], conj H[b] of the thread's outputs over this half's classes
 #pragma unroll
     for (int j = 0; j < OT; ++j) Ha[j] = Hb[j] = {0.f, 0.f};
@@ -206,27 +299,32 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
         uint32_t e[C2_SN];
         {  // every load of the class slice in one round trip; past the class's end s reads 0 and the
            // padded table points at the trash slot (sparc.py:429-432 below writes there harmlessly)
-            const __amdgpu_buffer_rsrc_t rs = c2_rsrc(s + q0, 4 * (q1 - q0));
+            const __amdgpu_buffer_rsrc_t rs0 = c2_rsrc(s + q0, 4 * (q1 - q0));
             const __amdgpu_buffer_rsrc_t re = c2_rsrc(tb.cls2 + (size_t)m2 * CW2_SLICE, 4 * CW2_SLICE);
 #pragma unroll
             for (int i = 0; i < C2_SN; ++i) {
-                v[i] = c2_ldf(rs, 4 * tl + 4 * i * C2_T, 0);
+                v[i] = c2_ldf(rs0, 4 * tl + 4 * i * C2_T, 0);
                 e[i] = c2_ldu(re, 4 * tl, 4 * i * C2_T);
             }
         }
+        const __amdgpu_buffer_rsrc_t rs = c2_rsrc(s + q0, 4 * (q1 - q0));
 #pragma unroll
-        for (int c = 0; c < C2_NC; ++c) {  // beta = eta(s), sparc.py:429-432, scattered into the image
+        for (int c = 0; c < C2_NC; ++c) {  // beta = eta(s), sparc.py:429-432, scattered into the image and
+                                           // stored over s for cw2_az (its beta_prev; past the end: dropped)
 #pragma unroll
             for (int i = c * C2_SC; i < (c + 1) * C2_SC; ++i) {
                 const int sec = e[i] >> 16;
-                dr[e[i] & 0xffffu] = __expf((v[i] - sM[sec]) * inv_tp) * sI[sec];
+                v[i] = __expf((v[i] - sM[sec]) * inv_tp) * sI[sec];
+                dr[e[i] & 0xffffu] = v[i];
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[i]), rs, 4 * tl + 4 * i * C2_T,
+                                                      0, 0);
             }
             C2_TPC(1 + c);
         }
         const uint32_t cmk = tb.cmask[m2 * C2_T + tl];
         __syncthreads();
         C2_TPC(3);
-        c2_fft<false>(d, tl, cmk);
+        c2_fft<false>(tl, cmk);
         C2_TPC(6);
         // H[a] += W Y[r], conj H[b] += W conj Y[P - r] (invalid slots: a = 0, unused); the
         // owned indices a reloaded per class (L1) rather than held across the transform
@@ -239,7 +337,8 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
             for (int j = 0; j < OT; ++j) {
                 const uint32_t a = ka[j] & CW_KMASK;
                 const int r = (int)a & (C2_P - 1);
-                const cx<float> ya = d[fsw(r)], yb = d[fsw((C2_P - r) & (C2_P - 1))];
+                const c2f ya2 = *c2_at(c2pos(r)), yb2 = *c2_at(c2pos((C2_P - r) & (C2_P - 1)));
+                const cx<float> ya = {ya2.x, ya2.y}, yb = {yb2.x, yb2.y};
                 const cx<float> w = c2_w(tb, (uint32_t)m2 * a);
                 Ha[j] = cmac_pk(Ha[j], w, ya);
                 Hb[j] = cmacc_pk(Hb[j], w, yb);
@@ -349,18 +448,11 @@ __global__ __launch_bounds__(C2_T) void cw2_ctrl(Cw2Tables tb, RegBufs<float> bf
 template <int OT>
 __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> bf, int t) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    cx<float> *d = reinterpret_cast<cx<float> *>(smem);
     float *dr = reinterpret_cast<float *>(smem);
-    float *sM = reinterpret_cast<float *>(smem + C2_IMG_BYTES), *sI = sM + 1024;
     const int h = blockIdx.x & 1, cw = blockIdx.x >> 1, tid = threadIdx.x;
     if (!bf.active[cw]) return;
     const size_t lb = (size_t)cw * tb.L;
     const bool have_beta = t > 0;
-    for (int l = tid; l < tb.L; l += C2_T) {  // previous beta's section max, 1/sum (t = 0: unused)
-        sM[l] = have_beta ? bf.stM[lb + l] : 0.f;
-        sI[l] = have_beta ? bf.stI[lb + l] : 0.f;
-    }
-    const float inv_tp = have_beta ? (float)(1.0 / bf.tau_prev[cw]) : 1.f;  // the previous beta's tau
     const double tv = bf.tau[cw];
     const float tau = (float)tv, inv_tau = (float)(1.0 / tv);
     float *s = bf.s + (size_t)cw * tb.LM;
@@ -410,10 +502,10 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
                 if (k & CW_ENDROW) {
                     const int r = (int)a & (C2_P - 1);
                     if (k & CW_SELF) {
-                        d[fsw(r)] = cadd(u0, u1);
+                        *c2_at(c2pos(r)) = c2f{u0.x + u1.x, u0.y + u1.y};
                     } else {
-                        d[fsw(r)] = u0;
-                        d[fsw(C2_P - r)] = u1;
+                        *c2_at(c2pos(r)) = c2f{u0.x, u0.y};
+                        *c2_at(c2pos(C2_P - r)) = c2f{u1.x, u1.y};
                     }
                 }
             }
@@ -421,7 +513,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
         C2_TPC(33);
         __syncthreads();
         C2_TPC(34);
-        c2_fft<true>(d, tl, rmk);
+        c2_fft<true>(tl, rmk);
         C2_TPC(35);
         const int q0 = c2_uni(tb.cls_ptr[m2]), q1 = c2_uni(tb.cls_ptr[m2 + 1]);
         float snv[C2_SN];
@@ -437,9 +529,8 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
                 v[i] = c2_ldf(rs, 4 * tl + 4 * i * C2_T, 0);  // (t = 0: unused)
             }
 #pragma unroll
-            for (int i = 0; i < C2_SN; ++i) {
-                const int sec = e[i] >> 16;
-                const float b = have_beta ? __expf((v[i] - sM[sec]) * inv_tp) * sI[sec] : 0.f;
+            for (int i = 0; i < C2_SN; ++i) {  // s = beta_prev + tau u (sparc.py:972); beta_prev stored by cw2_ab
+                const float b = have_beta ? v[i] : 0.f;
                 snv[i] = b + tau * dr[e[i] & 0xffffu];
             }
         }
@@ -598,6 +689,18 @@ template <int OT>
 static int cw2_launch(const Cw2Tables &tb, const RegBufs<float> &bf, const AmpScalars &sc, const AmpParams &pr,
                       int t, hipStream_t s) {
     const size_t lds = C2_LDS_BYTES;  // the P-point image (also the class copy: fpad(maxcls + 16) < 2 P), stM, stI
+    static const int ready = []() -> int {  // the image addresses assume no static LDS (c2_at)
+        hipFuncAttributes fa, fz;
+        if (hipFuncGetAttributes(&fa, (const void *)cw2_ab<OT>) != hipSuccess ||
+            hipFuncGetAttributes(&fz, (const void *)cw2_az<OT>) != hipSuccess || fa.sharedSizeBytes ||
+            fz.sharedSizeBytes)
+            return 0;
+        return hipFuncSetAttribute((const void *)cw2_ab<OT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)C2_LDS_BYTES) == hipSuccess &&
+               hipFuncSetAttribute((const void *)cw2_az<OT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)C2_LDS_BYTES) == hipSuccess;
+    }();
+    if (!ready) return fail(SG_ERR_HIP, "split per-codeword engine: kernel attributes (static LDS / LDS size)");
     const dim3 g2(2 * bf.B), gB(bf.B);
     if (t > 0) {
         ProfScope ps(SG_PH_CW2_AB, s);

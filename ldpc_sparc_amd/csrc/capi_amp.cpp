@@ -585,9 +585,15 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
     }
     // class tables padded to CW2_SLICE entries per class, the padding pointing
     // at the trash slot (section 0), so the kernels need no range checks
+    // (entries re-addressed from the one-workgroup engine's fsw image to the
+    // split engine's padded one, c2pos)
     std::vector<uint32_t> cls2((size_t)Q * CW2_SLICE, CW2_TRASH);
     for (int m2 = 0; m2 < Q; ++m2)
-        std::copy(cls_ls.begin() + cls_ptr[m2], cls_ls.begin() + cls_ptr[m2 + 1], cls2.begin() + (size_t)m2 * CW2_SLICE);
+        for (int q = cls_ptr[m2]; q < cls_ptr[m2 + 1]; ++q) {
+            const uint32_t loc = cls_ls[q] & 0xffffu;
+            const uint32_t pl = 2u * (uint32_t)c2pos(fsw((int)(loc >> 1))) + (loc & 1u);
+            cls2[(size_t)m2 * CW2_SLICE + (q - cls_ptr[m2])] = (cls_ls[q] & ~0xffffu) | pl;
+        }
     SG_TRY(upload(p, &p->c2_cls, cls2));
     SG_TRY(upload(p, &p->c2_cmask, cmask));
     SG_TRY(upload(p, &p->c2_ka, ka));
