@@ -550,39 +550,61 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
         __syncthreads();
         C2_TPC(38);
 #pragma unroll
-        for (int c = 0; c < C2_SN; ++c) dr[fpad(tl + c * C2_T)] = snv[c];  // s of the class in class order,
-                                                                           // skewed by fpad (past the end: unread)
+        for (int c = 0; c < C2_SN; ++c) dr[tl + c * C2_T] = snv[c];  // s of the class in class order (past the
+                                                                     // end: unread)
         __syncthreads();
         C2_TPC(39);
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             // partial of the section over its segment: the maximum and its first
             // position, then the sums of e and e^2 over the other entries
-            // (e = exp((x - max) / tau)); two passes over the class copy with
-            // selects instead of the online rescaling (fewer vector instructions)
+            // (e = exp((x - max) / tau)); two passes with selects instead of the
+            // online rescaling (fewer vector instructions).  The first 16
+            // entries are read once for both passes (segments average
+            // LM / (Q L) = 8 entries; longer ones take the loops below), the
+            // reads are unskewed (every read a base plus a constant; the
+            // segment starts are irregular either way) and entries past the
+            // segment read as -inf (exp -> 0).
             const int a = sa[k], n = sb[k] - sa[k];
             constexpr int RC = 16;
+            const float *sgp = dr + a;  // inside the LDS image past the segment's end too
+            float x[RC];
+#pragma unroll
+            for (int i = 0; i < RC; ++i) x[i] = i < n ? sgp[i] : -INFINITY;
             float m = -INFINITY;
             int am = -1;
-            for (int c = 0; c < n; c += RC) {
-                float x[RC];
 #pragma unroll
-                for (int i = 0; i < RC; ++i) x[i] = dr[fpad(a + c + i)];  // inside the LDS image; masked below
+            for (int i = 0; i < RC; ++i) {
+                const bool up = x[i] > m;
+                m = up ? x[i] : m;
+                am = up ? i : am;
+            }
+            for (int c = RC; c < n; c += RC) {
+                float y[RC];
+#pragma unroll
+                for (int i = 0; i < RC; ++i) y[i] = dr[a + c + i];
 #pragma unroll
                 for (int i = 0; i < RC; ++i) {
-                    const bool up = c + i < n && x[i] > m;
-                    m = up ? x[i] : m;
+                    const bool up = c + i < n && y[i] > m;
+                    m = up ? y[i] : m;
                     am = up ? c + i : am;
                 }
             }
             float S1 = 0.f, S2 = 0.f;
-            for (int c = 0; c < n; c += RC) {
-                float x[RC];
 #pragma unroll
-                for (int i = 0; i < RC; ++i) x[i] = dr[fpad(a + c + i)];
+            for (int i = 0; i < RC; ++i) {
+                float ex = __expf((x[i] - m) * inv_tau);
+                ex = i != am ? ex : 0.f;
+                S1 += ex;
+                S2 += ex * ex;
+            }
+            for (int c = RC; c < n; c += RC) {
+                float y[RC];
+#pragma unroll
+                for (int i = 0; i < RC; ++i) y[i] = dr[a + c + i];
 #pragma unroll
                 for (int i = 0; i < RC; ++i) {
-                    float ex = __expf((x[i] - m) * inv_tau);
+                    float ex = __expf((y[i] - m) * inv_tau);
                     ex = (c + i < n && c + i != am) ? ex : 0.f;
                     S1 += ex;
                     S2 += ex * ex;
@@ -600,7 +622,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
                     R2[k] += (1.f + S2) * (f * f);
                 }
             }
-            if (jt[k] >= q0 && jt[k] < q1) st[k] = dr[fpad(jt[k] - q0)];
+            if (jt[k] >= q0 && jt[k] < q1) st[k] = dr[jt[k] - q0];
         }
         C2_TPC(40);
         __syncthreads();  // the next class overwrites the image
