@@ -69,21 +69,36 @@ typedef float c2f __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) c2f c2lds;
 __device__ __forceinline__ c2lds *c2_at(int pos) { return (c2lds *)(size_t)(8u * (uint32_t)pos); }
 
+// The packed instructions' modifiers negate whole operands, and the compiler
+// does not fold a one-lane negation into them (it spends a xor and a move on
+// each {-y, x} pair), so every sign pattern is a constant pair: one packed
+// multiply or FMA by (1, -1) / (-1, 1).
+__device__ __forceinline__ c2f c2_pm() { return c2f{1.f, -1.f}; }
+__device__ __forceinline__ c2f c2_mp() { return c2f{-1.f, 1.f}; }
 template <bool INV>
 __device__ __forceinline__ c2f c2_mi(c2f a) {  // * -i (forward), * +i (inverse)
-    return INV ? c2f{-a.y, a.x} : c2f{a.y, -a.x};
+    return a.yx * (INV ? c2_mp() : c2_pm());
 }
-__device__ __forceinline__ c2f c2_mul(c2f a, c2f w) {  // two packed instructions
-    return __builtin_elementwise_fma(c2f{-a.y, a.y}, w.yx, a.xx * w);
+// x + (* -i or * +i)(d) in one packed FMA
+template <bool INV>
+__device__ __forceinline__ c2f c2_addmi(c2f x, c2f d) {
+    return __builtin_elementwise_fma(d.yx, INV ? c2_mp() : c2_pm(), x);
+}
+template <bool INV>
+__device__ __forceinline__ c2f c2_submi(c2f x, c2f d) {
+    return __builtin_elementwise_fma(d.yx, INV ? c2_pm() : c2_mp(), x);
+}
+__device__ __forceinline__ c2f c2_mul(c2f a, c2f w) {  // three packed instructions
+    return __builtin_elementwise_fma(a.yy * w.yx, c2_mp(), a.xx * w);
 }
 
 template <bool INV>
 __device__ __forceinline__ void c2_dft4(c2f &a0, c2f &a1, c2f &a2, c2f &a3) {
-    const c2f t0 = a0 + a2, t1 = a0 - a2, t2 = a1 + a3, t3 = c2_mi<INV>(a1 - a3);
+    const c2f t0 = a0 + a2, t1 = a0 - a2, t2 = a1 + a3, d = a1 - a3;
     a0 = t0 + t2;
     a2 = t0 - t2;
-    a1 = t1 + t3;
-    a3 = t1 - t3;
+    a1 = c2_addmi<INV>(t1, d);
+    a3 = c2_submi<INV>(t1, d);
 }
 
 // 16-point DFT as 4 x 4 (fft.hpp dft16: inputs n = 4 n1 + n2, outputs k = k1 + 4 k2)
@@ -102,7 +117,7 @@ __device__ __forceinline__ void c2_dft16(c2f *a) {
     }
     // y[n2][k1] *= w16^(n2 k1): x (c - i s) forward, x (c + i s) inverse
     auto tw = [&](c2f x, float c, float s) -> c2f {
-        return __builtin_elementwise_fma(INV ? c2f{-x.y, x.x} : c2f{x.y, -x.x}, c2f{s, s}, x * c2f{c, c});
+        return __builtin_elementwise_fma(x.yx, INV ? c2f{-s, s} : c2f{s, -s}, x * c2f{c, c});
     };
     y[1][1] = tw(y[1][1], c1, s1);
     y[1][2] = tw(y[1][2], r2, r2);
