@@ -219,6 +219,9 @@ struct Cw2Tables {
     const int32_t *qpos;      // [Mc]
     const uint16_t *seg;      // [Q][Lblk+1]
     float4 *xp;               // [B][2][OT][512] partial (H[a], conj H[b]) of each half
+    const uint2 *rab;         // [OT][512] LDS byte addresses of rows r, P - r of the slot's output (cw2_ab reads)
+    const uint2 *wab;         // [OT][512] LDS byte addresses of the slot's row writes (rows r, P - r on the
+                              // pair's last slot, else the trash slot; r = 0, P / 2: row r and trash)
     float *vz;                // [B][OT][512] z / phi in slot order
     float4 *part;             // [B][2][Lblk] partial section statistics (max, R1, R2, s of the true entry or NaN)
     uint64_t *tprof;          // diagnostics (SG_AMP_TPROF): [2 B][64] shader-clock stamps (Ab 0-31, Az 32-63), or null

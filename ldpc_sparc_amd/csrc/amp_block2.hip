@@ -29,6 +29,7 @@ namespace sg {
 constexpr int B2_THREADS = 1024;
 constexpr int B2_LOG2P = 14, B2_P = 1 << B2_LOG2P;
 constexpr int B2_J = 32;  // column entries per thread (Mc = 32768)
+constexpr int B2_JR = 24;  // of which blk2_ab holds in registers (the other 8 in LDS: 32 KB)
 
 namespace {
 
@@ -83,7 +84,8 @@ __device__ __forceinline__ uint32_t b2_pos(const uint32_t *pv, int i) { return (
 
 // the first three stages (radix 16) of the P-point FFT, as amp_block.hip
 __device__ __forceinline__ void b2_fwd_stages(cx<float> *d, const cx<float> *__restrict__ stw, int tid) {
-    if constexpr (SG_BLK_SINCOS & 1) {
+    if constexpr (true) {  // sine / cosine twiddles: no table entries in flight (blk2_ab holds beta_c in
+                           // registers; with the table prefetch it spills)
         lds_fft1_sincos<false, 16, B2_LOG2P, 0, 3>(d, tid);
     } else {
         cx<float> w0[1], w1[6], w2[6];
@@ -97,7 +99,7 @@ __device__ __forceinline__ void b2_fwd_stages(cx<float> *d, const cx<float> *__r
 
 }  // namespace
 
-size_t blk2_lds_bytes() { return (size_t)B2_P * sizeof(cx<float>); }
+size_t blk2_lds_bytes() { return (size_t)B2_P * sizeof(cx<float>) + (size_t)(B2_J - B2_JR) * B2_THREADS * 4; }
 
 // ------------------------------------------------------------------ Ab
 template <int EPS>
@@ -108,15 +110,23 @@ __global__ __launch_bounds__(B2_THREADS) void blk2_ab(BlkTables tb, AmpBufs<floa
     const int c = blockIdx.x, cw = blockIdx.y, tid = threadIdx.x;
     if (!bf.active[cw]) return;
     const float *beta = bf.beta + (size_t)cw * tb.LM + (size_t)c * tb.Mc;
+    // beta_c read once for all the column's transforms and classes: entries
+    // 0..B2_JR-1 of the thread in registers, the rest in the LDS past the image
+    // (all in registers spills around the transform)
+    float bv[B2_JR];
+    float *bx = reinterpret_cast<float *>(smem + (size_t)B2_P * sizeof(cx<float>));
+#pragma unroll
+    for (int i = 0; i < B2_J; ++i) {
+        const float b = beta[b2_j<EPS>(tid, i)];
+        if (i < B2_JR) bv[i < B2_JR ? i : 0] = b;
+        else bx[(i - B2_JR) * B2_THREADS + tid] = b;
+    }
     for (int q = tb.col_ptr[c]; q < tb.col_ptr[c + 1]; ++q) {
         const int t = tb.col_t[q];
         float acc = 0.f;  // output tid (Mr <= 1024), summed over the two classes
         for (int m2 = 0; m2 < 2; ++m2) {
             const int tl = b2_opaque(tid);
-            // beta_c and the positions, in flight while the image clears
-            float bv[B2_J];
-#pragma unroll
-            for (int i = 0; i < B2_J; ++i) bv[i] = beta[b2_j<EPS>(tl, i)];
+            // the positions, in flight while the image clears
             uint32_t pv[B2_J / 2];
             b2_pos_load(tb, t, tl, pv);
             b2_clear(smem, tl);
@@ -124,7 +134,8 @@ __global__ __launch_bounds__(B2_THREADS) void blk2_ab(BlkTables tb, AmpBufs<floa
 #pragma unroll
             for (int i = 0; i < B2_J; ++i) {
                 const uint32_t p = b2_pos(pv, i);
-                if ((int)(p >> 15) == m2) dr[p & 0x7fffu] = bv[i];
+                const float b = i < B2_JR ? bv[i < B2_JR ? i : 0] : bx[(i - B2_JR) * B2_THREADS + tl];
+                if ((int)(p >> 15) == m2) dr[p & 0x7fffu] = b;
             }
             __syncthreads();
             b2_fwd_stages(d, tb.stw, tl);

@@ -68,6 +68,19 @@ __device__ __forceinline__ cx<float> c2_w(const Cw2Tables &tb, uint32_t j) {
 typedef float c2f __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) c2f c2lds;
 __device__ __forceinline__ c2lds *c2_at(int pos) { return (c2lds *)(size_t)(8u * (uint32_t)pos); }
+// complex index of the first radix-16 stage's twiddle table (after the image,
+// the staged statistics and the trash slot): w_512^(r k) at (r - 1) 32 + k,
+// r = 1..15, k < 32, forward or (cw2_az) inverse
+constexpr int C2_TW1 = ((8192 + 256) * 8 + 2 * 1024 * 4 + 16) / 8;
+template <bool INV>
+__device__ __forceinline__ void c2_tw1_init(int tid) {
+    for (int i = tid; i < 15 * 32; i += C2_T) {
+        const int r = i / 32 + 1, k = i & 31;
+        const float x = (float)((r * k) & 511) * (1.0f / 512.0f);
+        const float sn = __builtin_amdgcn_sinf(x);
+        *c2_at(C2_TW1 + i) = c2f{__builtin_amdgcn_cosf(x), INV ? sn : -sn};
+    }
+}
 
 // The packed instructions' modifiers negate whole operands, and the compiler
 // does not fold a one-lane negation into them (it spends a xor and a move on
@@ -214,7 +227,11 @@ __device__ __forceinline__ void c2_stage_r16(int tid) {
     const c2lds *src = c2_at(j + (j >> 5));  // c2pos(j + 512 r) = c2pos(j) + 528 r
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = src[528 * r];
-    {
+    if constexpr (NS == 32) {  // the 15 x 32 twiddles of this stage from the workgroup's LDS table
+        const c2lds *tw = c2_at(C2_TW1 + k);
+#pragma unroll
+        for (int r = 1; r < 16; ++r) v[r] = c2_mul(v[r], tw[32 * (r - 1)]);
+    } else {
         constexpr float inv = 1.0f / (float)(16 * NS);
         const float x1 = (float)k * inv, x4 = (float)((4 * k) & (16 * NS - 1)) * inv;
         const c2f w1 = c2f{__builtin_amdgcn_cosf(x1), INV ? __builtin_amdgcn_sinf(x1) : -__builtin_amdgcn_sinf(x1)};
@@ -264,7 +281,9 @@ __device__ __forceinline__ void c2_fft(int tid, uint32_t msk) {
 // LDS: the P-point image (64 KB), then the previous beta's section max and
 // 1/sum (stM, stI: 8 KB), staged once per launch.
 constexpr size_t C2_IMG_BYTES = (size_t)c2pos(C2_P) * 8;  // padded: element i at c2pos(i)
-constexpr size_t C2_LDS_BYTES = C2_IMG_BYTES + 2 * 1024 * 4 + 16;  // + the trash slot (CW2_TRASH)
+constexpr size_t C2_LDS_BYTES = C2_IMG_BYTES + 2 * 1024 * 4 + 16 + 15 * 32 * 8;  // + the trash slot (CW2_TRASH),
+                                                                                // the stage twiddles (C2_TW1)
+static_assert(C2_TW1 * 8 == C2_IMG_BYTES + 2 * 1024 * 4 + 16, "twiddle table after the trash slot");
 static_assert(CW2_TRASH == (C2_IMG_BYTES + 2 * 1024 * 4) / 4, "trash slot after the staged statistics");
 
 // Raw buffer resources: loads and stores address by a per-lane byte offset
@@ -290,13 +309,12 @@ template <int OT>
 __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> bf) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float *dr = reinterpret_cast<float *>(smem);
-    float *sM = reinterpret_cast<float *>(smem + C2_IMG_BYTES), *sI = sM + 1024;
+    c2f *sMI = reinterpret_cast<c2f *>(smem + C2_IMG_BYTES);  // previous beta's (section max, 1 / sum)
     const int h = blockIdx.x & 1, cw = blockIdx.x >> 1, tid = threadIdx.x;
     if (!bf.active[cw]) return;
     const size_t lb = (size_t)cw * tb.L;
     for (int l = tid; l < tb.L; l += C2_T) {  // previous beta's section max, 1/sum
-        sM[l] = bf.stM[lb + l];
-        sI[l] = bf.stI[lb + l];
+        sMI[l] = c2f{bf.stM[lb + l], bf.stI[lb + l]};
     }
     const float inv_tp = (float)(1.0 / bf.tau[cw]);
     float *s = bf.s + (size_t)cw * tb.LM;  // s in; beta out (read by cw2_az, which writes the new s)
@@ -304,6 +322,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
 #pragma unroll
     for (int j = 0; j < OT; ++j) Ha[j] = Hb[j] = {0.f, 0.f};
     const int Qh = tb.Q >> 1;
+    c2_tw1_init<false>(tid);
     __syncthreads();  // the staged statistics
     C2_TP(10);
     for (int m2 = h * Qh; m2 < (h + 1) * Qh; ++m2) {
@@ -329,7 +348,8 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
 #pragma unroll
             for (int i = c * C2_SC; i < (c + 1) * C2_SC; ++i) {
                 const int sec = e[i] >> 16;
-                v[i] = __expf((v[i] - sM[sec]) * inv_tp) * sI[sec];
+                const c2f mi = sMI[sec];
+                v[i] = __expf((v[i] - mi.x) * inv_tp) * mi.y;
                 dr[e[i] & 0xffffu] = v[i];
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[i]), rs, 4 * tl + 4 * i * C2_T,
                                                       0, 0);
@@ -343,20 +363,30 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
         C2_TPC(6);
         // H[a] += W Y[r], conj H[b] += W conj Y[P - r] (invalid slots: a = 0, unused); the
         // owned indices a reloaded per class (L1) rather than held across the transform
+        // (the rows' LDS byte addresses from the host table rab, in two rounds)
         {
-            uint32_t ka[OT];
-            const __amdgpu_buffer_rsrc_t rk = c2_rsrc(tb.ka, 4 * OT * C2_T);
+            constexpr int CH = (OT + 1) / 2;
+            const __amdgpu_buffer_rsrc_t rk = c2_rsrc(tb.ka, 4 * OT * C2_T), rr = c2_rsrc(tb.rab, 8 * OT * C2_T);
 #pragma unroll
-            for (int j = 0; j < OT; ++j) ka[j] = c2_ldu(rk, 4 * c2_opaque(tl), 4 * j * C2_T);
+            for (int j0 = 0; j0 < OT; j0 += CH) {
+                uint32_t ka[CH];
+                uint2 ra[CH];
 #pragma unroll
-            for (int j = 0; j < OT; ++j) {
-                const uint32_t a = ka[j] & CW_KMASK;
-                const int r = (int)a & (C2_P - 1);
-                const c2f ya2 = *c2_at(c2pos(r)), yb2 = *c2_at(c2pos((C2_P - r) & (C2_P - 1)));
-                const cx<float> ya = {ya2.x, ya2.y}, yb = {yb2.x, yb2.y};
-                const cx<float> w = c2_w(tb, (uint32_t)m2 * a);
-                Ha[j] = cmac_pk(Ha[j], w, ya);
-                Hb[j] = cmacc_pk(Hb[j], w, yb);
+                for (int i = 0; i < CH; ++i) {
+                    ka[i] = c2_ldu(rk, 4 * c2_opaque(tl), 4 * (j0 + i) * C2_T);
+                    ra[i] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rr, 8 * tl, 8 * (j0 + i) * C2_T, 0));
+                }
+#pragma unroll
+                for (int i = 0; i < CH; ++i) {
+                    const int j = j0 + i;
+                    if (j >= OT) break;
+                    const uint32_t a = ka[i] & CW_KMASK;
+                    const c2f ya2 = *(const c2lds *)(size_t)ra[i].x, yb2 = *(const c2lds *)(size_t)ra[i].y;
+                    const cx<float> ya = {ya2.x, ya2.y}, yb = {yb2.x, yb2.y};
+                    const cx<float> w = c2_w(tb, __umul24((uint32_t)m2, a));  // (a < 2^19, m2 < 2^6: full-rate multiply)
+                    Ha[j] = cmac_pk(Ha[j], w, ya);
+                    Hb[j] = cmacc_pk(Hb[j], w, yb);
+                }
             }
         }
         C2_TPC(8);
@@ -482,46 +512,50 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
         if (bf.true_idx && sec < Lb) jt[k] = tb.qpos[sec * tb.M + bf.true_idx[lb + sec]];
     }
     const int Qh = tb.Q >> 1;
+    c2_tw1_init<true>(tid);
     __syncthreads();  // the staged statistics
     C2_TP(42);
     for (int m2 = h * Qh; m2 < (h + 1) * Qh; ++m2) {
         const int tl = c2_opaque(tid);
         C2_TPC(32);
         const uint32_t rmk = tb.cmask[tb.Q * C2_T + tl];
-        {  // rows r and P - r of each owned pair: sum of al v conj(W) / be v W over its outputs
-           // (a, v = z / phi, al, be reloaded per class from L1 / L2: held across the transform, or
-           // loaded one class ahead, they spill)
-            cx<float> g1[OT], g2[OT];
-            uint32_t ka[OT];
+        {  // rows r and P - r of each owned pair: sum of al v conj(W) / be v W over its outputs (v = z / phi),
+           // branch-free: every slot accumulates (NEWROW restarts the sums) and writes both rows, at the
+           // addresses of the host table wab -- the pair's rows on its last slot, the trash slot otherwise
+           // (invalid slots: al = be = 0); the two pairs whose rows coincide (r = 0, P / 2) then write their
+           // sum.  (a, al, be, v and the addresses reloaded per class from L1 / L2: held across the transform,
+           // or loaded one class ahead, they spill; al v and be v precomputed per codeword were slower -- four
+           // times the per-codeword bytes re-read from L2 every class.)
+            constexpr int CH = OT > 12 ? (OT + 1) / 2 : OT;  // slots per load round (all of them at 12 per thread)
             const __amdgpu_buffer_rsrc_t rg = c2_rsrc(tb.gf, 16 * OT * C2_T), rv = c2_rsrc(vz, 4 * OT * C2_T),
-                                         rk = c2_rsrc(tb.ka, 4 * OT * C2_T);
-#pragma unroll
-            for (int j = 0; j < OT; ++j) {
-                ka[j] = c2_ldu(rk, 4 * tl, 4 * j * C2_T);
-                const float4 gc = __builtin_bit_cast(
-                    float4, __builtin_amdgcn_raw_buffer_load_b128(rg, 16 * tl, 16 * j * C2_T, 0));
-                const float vv = c2_ldf(rv, 4 * tl, 4 * j * C2_T);
-                g1[j] = {gc.x * vv, gc.y * vv};
-                g2[j] = {gc.z * vv, gc.w * vv};
-            }
+                                         rk = c2_rsrc(tb.ka, 4 * OT * C2_T), rw = c2_rsrc(tb.wab, 8 * OT * C2_T);
             cx<float> u0{0.f, 0.f}, u1{0.f, 0.f};
 #pragma unroll
-            for (int j = 0; j < OT; ++j) {
-                const uint32_t k = ka[j];
-                if (!(k & CW_VALID)) continue;
-                const uint32_t a = k & CW_KMASK;
-                const cx<float> w = c2_w(tb, (uint32_t)m2 * a);
-                if (k & CW_NEWROW) u0 = u1 = {0.f, 0.f};
-                u0 = cmacc_pk(u0, g1[j], w);
-                u1 = cmac_pk(u1, g2[j], w);
-                if (k & CW_ENDROW) {
-                    const int r = (int)a & (C2_P - 1);
-                    if (k & CW_SELF) {
-                        *c2_at(c2pos(r)) = c2f{u0.x + u1.x, u0.y + u1.y};
-                    } else {
-                        *c2_at(c2pos(r)) = c2f{u0.x, u0.y};
-                        *c2_at(c2pos(C2_P - r)) = c2f{u1.x, u1.y};
-                    }
+            for (int j0 = 0; j0 < OT; j0 += CH) {
+                uint32_t ka[CH];
+                float4 gc[CH];
+                float vv[CH];
+                uint2 wa[CH];
+#pragma unroll
+                for (int i = 0; i < CH; ++i) {
+                    const int j = j0 + i < OT ? j0 + i : OT - 1;
+                    ka[i] = c2_ldu(rk, 4 * tl, 4 * j * C2_T);
+                    gc[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, 16 * tl, 16 * j * C2_T, 0));
+                    vv[i] = c2_ldf(rv, 4 * tl, 4 * j * C2_T);
+                    wa[i] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rw, 8 * tl, 8 * j * C2_T, 0));
+                }
+#pragma unroll
+                for (int j = 0; j < CH; ++j) {
+                    if (j0 + j >= OT) break;
+                    const uint32_t k = ka[j];
+                    const cx<float> w = c2_w(tb, __umul24((uint32_t)m2, k & CW_KMASK));  // (a < 2^19, m2 < 2^6)
+                    const float keep = (k & CW_NEWROW) ? 0.f : 1.f;
+                    u0 = cmacc_pk({u0.x * keep, u0.y * keep}, {gc[j].x * vv[j], gc[j].y * vv[j]}, w);
+                    u1 = cmac_pk({u1.x * keep, u1.y * keep}, {gc[j].z * vv[j], gc[j].w * vv[j]}, w);
+                    c2lds *pa = (c2lds *)(size_t)wa[j].x, *pb = (c2lds *)(size_t)wa[j].y;
+                    *pa = c2f{u0.x, u0.y};
+                    *pb = c2f{u1.x, u1.y};
+                    if (k & CW_SELF) *pa = c2f{u0.x + u1.x, u0.y + u1.y};
                 }
             }
         }

@@ -72,6 +72,7 @@ struct sg_amp_plan {
     int cw2OT = 0;
     uint32_t *c2_ka = nullptr, *c2_cmask = nullptr, *c2_cls = nullptr;
     int32_t *c2_oi = nullptr;
+    uint32_t *c2_wab = nullptr, *c2_rab = nullptr;
     void *c2_cf = nullptr, *c2_gf = nullptr;
     void *ws_c2xp = nullptr, *ws_c2vz = nullptr, *ws_c2part = nullptr;
     uint16_t *c_cmask = nullptr;  // [Q + 1][1024] per-codeword engine: written image values per thread
@@ -543,6 +544,7 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
     std::vector<uint32_t> ka((size_t)OT * T, 0u);
     std::vector<int32_t> oi((size_t)OT * T, 0);
     std::vector<float> cf((size_t)OT * T * 4, 0.f), gf((size_t)OT * T * 4, 0.f);
+    std::vector<uint32_t> wab((size_t)OT * T * 2, 4u * CW2_TRASH), rab((size_t)OT * T * 2, 0u);
     for (int tid = 0; tid < T; ++tid) {
         int j = 0;
         for (int r : own[tid]) {
@@ -556,6 +558,12 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
                 if (r == 0 || 2 * r == P) e |= CW_SELF;
                 const size_t c = (size_t)j * T + tid;
                 ka[c] = e;
+                rab[2 * c] = 8u * (uint32_t)c2pos(r);
+                rab[2 * c + 1] = 8u * (uint32_t)c2pos((P - r) % P);
+                if (q + 1 == lst.size()) {  // the pair's row writes (amp_cw2.hip Az rows)
+                    wab[2 * c] = 8u * (uint32_t)c2pos(r);
+                    wab[2 * c + 1] = (e & CW_SELF) ? 4u * CW2_TRASH : 8u * (uint32_t)c2pos(P - r);
+                }
                 oi[c] = i;
                 const float v[8] = {(float)o.c1.real(), (float)o.c1.imag(), (float)o.c2.real(), (float)o.c2.imag(),
                                     (float)o.al.real(), (float)o.al.imag(), (float)o.be.real(), (float)o.be.imag()};
@@ -598,6 +606,8 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
     SG_TRY(upload(p, &p->c2_cmask, cmask));
     SG_TRY(upload(p, &p->c2_ka, ka));
     SG_TRY(upload(p, &p->c2_oi, oi));
+    SG_TRY(upload(p, &p->c2_wab, wab));
+    SG_TRY(upload(p, &p->c2_rab, rab));
     float *dcf = nullptr, *dgf = nullptr;
     SG_TRY(upload(p, &dcf, cf));
     SG_TRY(upload(p, &dgf, gf));
@@ -890,7 +900,7 @@ static Cw2Tables c2tables(const sg_amp_plan *p) {
     tb.cmask = p->c2_cmask; tb.ka = p->c2_ka; tb.oi = p->c2_oi;
     tb.cf = (const float4 *)p->c2_cf; tb.gf = (const float4 *)p->c2_gf;
     tb.cls_ptr = p->r_cls_ptr; tb.cls_ls = p->r_cls_ls; tb.cls2 = p->c2_cls; tb.qpos = p->r_qpos; tb.seg = p->r_seg;
-    tb.xp = (float4 *)p->ws_c2xp; tb.vz = (float *)p->ws_c2vz; tb.part = (float4 *)p->ws_c2part;
+    tb.xp = (float4 *)p->ws_c2xp; tb.vz = (float *)p->ws_c2vz; tb.wab = (const uint2 *)p->c2_wab; tb.rab = (const uint2 *)p->c2_rab; tb.part = (float4 *)p->ws_c2part;
     tb.tprof = p->tprof;  // [2 B][64] stamps (the buffer holds B * Q * 20 >= 128 B words)
     return tb;
 }
