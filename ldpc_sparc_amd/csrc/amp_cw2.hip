@@ -281,8 +281,16 @@ __device__ __forceinline__ void c2_fft(int tid, uint32_t msk) {
 // LDS: the P-point image (64 KB), then the previous beta's section max and
 // 1/sum (stM, stI: 8 KB), staged once per launch.
 constexpr size_t C2_IMG_BYTES = (size_t)c2pos(C2_P) * 8;  // padded: element i at c2pos(i)
-constexpr size_t C2_LDS_BYTES = C2_IMG_BYTES + 2 * 1024 * 4 + 16 + 15 * 32 * 8;  // + the trash slot (CW2_TRASH),
-                                                                                // the stage twiddles (C2_TW1)
+constexpr size_t C2_CP_BYTES = C2_IMG_BYTES + 2 * 1024 * 4 + 16 + 15 * 32 * 8;  // class pointers (c2_stage_cp)
+constexpr size_t C2_LDS_BYTES = C2_CP_BYTES + 4 * 72;  // + the trash slot (CW2_TRASH), the stage twiddles
+                                                       // (C2_TW1), the class pointers (Q + 1 <= 72)
+// The class bounds from LDS: read through vector memory they made every class start wait for all
+// outstanding vector-memory operations (vmcnt(0)), the previous class's stores included.
+__device__ __forceinline__ const int *c2_stage_cp(unsigned char *smem, const Cw2Tables &tb, int tid) {
+    int *cp = reinterpret_cast<int *>(smem + C2_CP_BYTES);
+    for (int i = tid; i <= tb.Q; i += C2_T) cp[i] = tb.cls_ptr[i];
+    return cp;
+}
 static_assert(C2_TW1 * 8 == C2_IMG_BYTES + 2 * 1024 * 4 + 16, "twiddle table after the trash slot");
 static_assert(CW2_TRASH == (C2_IMG_BYTES + 2 * 1024 * 4) / 4, "trash slot after the staged statistics");
 
@@ -323,12 +331,48 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
     for (int j = 0; j < OT; ++j) Ha[j] = Hb[j] = {0.f, 0.f};
     const int Qh = tb.Q >> 1;
     c2_tw1_init<false>(tid);
+    const int *cpl = c2_stage_cp(smem, tb, tid);
     __syncthreads();  // the staged statistics
     C2_TP(10);
+    // H[a] += W Y[r], conj H[b] += W conj Y[P - r] from the image's transform of class m (invalid slots:
+    // a = 0, unused); the owned indices a and the rows' LDS byte addresses (host table rab) reloaded per
+    // class from L1 (held across the transform they spill), in two rounds
+    const __amdgpu_buffer_rsrc_t rk = c2_rsrc(tb.ka, 4 * OT * C2_T);
+    auto acc_tables = [&](int tl, uint32_t *ka) {
+#pragma unroll
+        for (int j = 0; j < OT; ++j) ka[j] = c2_ldu(rk, 4 * tl, 4 * j * C2_T);
+    };
+    auto accumulate = [&](int m, const uint32_t *ka) {
+#pragma unroll
+        for (int j = 0; j < OT; ++j) {
+            const uint32_t a = ka[j] & CW_KMASK;
+            const int r = (int)a & (C2_P - 1);
+            const c2f ya2 = *c2_at(c2pos(r)), yb2 = *c2_at(c2pos((C2_P - r) & (C2_P - 1)));
+            const cx<float> ya = {ya2.x, ya2.y}, yb = {yb2.x, yb2.y};
+            const cx<float> w = c2_w(tb, __umul24((uint32_t)m, a));  // (a < 2^19, m < 2^6: full-rate multiply)
+            Ha[j] = cmac_pk(Ha[j], w, ya);
+            Hb[j] = cmacc_pk(Hb[j], w, yb);
+        }
+    };
+    // Software-pipelined over the classes: class m2's slice is requested, then the previous class's
+    // transform (still in the image) is accumulated while the loads are in flight, then m2 is scattered
+    // and transformed
     for (int m2 = h * Qh; m2 < (h + 1) * Qh; ++m2) {
         const int tl = c2_opaque(tid);
         C2_TPC(0);
-        const int q0 = c2_uni(tb.cls_ptr[m2]), q1 = c2_uni(tb.cls_ptr[m2 + 1]);
+        const int q0 = c2_uni(cpl[m2]), q1 = c2_uni(cpl[m2 + 1]);
+        // (at more than 12 outputs per thread the slice is requested after the accumulation: in flight
+        // during it, it spills)
+        constexpr bool PL = OT <= 12;
+        if (!PL && m2 > h * Qh) {
+            uint32_t ka[OT];
+            acc_tables(tl, ka);
+            accumulate(m2 - 1, ka);
+            __syncthreads();
+        }
+        // (the accumulation's table loads first: vector-memory loads complete in order)
+        uint32_t ka[PL ? OT : 1];
+        if (PL && m2 > h * Qh) acc_tables(tl, ka);
         float v[C2_SN];
         uint32_t e[C2_SN];
         {  // every load of the class slice in one round trip; past the class's end s reads 0 and the
@@ -341,6 +385,13 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
                 e[i] = c2_ldu(re, 4 * tl, 4 * i * C2_T);
             }
         }
+        // (requested before the scatter's stores: a later load would wait for them, vmcnt is in order)
+        const uint32_t cmk = tb.cmask[m2 * C2_T + tl];
+        if (PL && m2 > h * Qh) {
+            accumulate(m2 - 1, ka);
+            __syncthreads();  // the image is read before the scatter overwrites it
+        }
+        C2_TPC(8);
         const __amdgpu_buffer_rsrc_t rs = c2_rsrc(s + q0, 4 * (q1 - q0));
 #pragma unroll
         for (int c = 0; c < C2_NC; ++c) {  // beta = eta(s), sparc.py:429-432, scattered into the image and
@@ -356,42 +407,15 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
             }
             C2_TPC(1 + c);
         }
-        const uint32_t cmk = tb.cmask[m2 * C2_T + tl];
         __syncthreads();
         C2_TPC(3);
         c2_fft<false>(tl, cmk);
         C2_TPC(6);
-        // H[a] += W Y[r], conj H[b] += W conj Y[P - r] (invalid slots: a = 0, unused); the
-        // owned indices a reloaded per class (L1) rather than held across the transform
-        // (the rows' LDS byte addresses from the host table rab, in two rounds)
-        {
-            constexpr int CH = (OT + 1) / 2;
-            const __amdgpu_buffer_rsrc_t rk = c2_rsrc(tb.ka, 4 * OT * C2_T), rr = c2_rsrc(tb.rab, 8 * OT * C2_T);
-#pragma unroll
-            for (int j0 = 0; j0 < OT; j0 += CH) {
-                uint32_t ka[CH];
-                uint2 ra[CH];
-#pragma unroll
-                for (int i = 0; i < CH; ++i) {
-                    ka[i] = c2_ldu(rk, 4 * c2_opaque(tl), 4 * (j0 + i) * C2_T);
-                    ra[i] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rr, 8 * tl, 8 * (j0 + i) * C2_T, 0));
-                }
-#pragma unroll
-                for (int i = 0; i < CH; ++i) {
-                    const int j = j0 + i;
-                    if (j >= OT) break;
-                    const uint32_t a = ka[i] & CW_KMASK;
-                    const c2f ya2 = *(const c2lds *)(size_t)ra[i].x, yb2 = *(const c2lds *)(size_t)ra[i].y;
-                    const cx<float> ya = {ya2.x, ya2.y}, yb = {yb2.x, yb2.y};
-                    const cx<float> w = c2_w(tb, __umul24((uint32_t)m2, a));  // (a < 2^19, m2 < 2^6: full-rate multiply)
-                    Ha[j] = cmac_pk(Ha[j], w, ya);
-                    Hb[j] = cmacc_pk(Hb[j], w, yb);
-                }
-            }
-        }
-        C2_TPC(8);
-        __syncthreads();
-        C2_TPC(9);
+    }
+    {
+        uint32_t ka[OT];
+        acc_tables(c2_opaque(tid), ka);
+        accumulate((h + 1) * Qh - 1, ka);
     }
     C2_TP(11);
     float4 *xp = tb.xp + ((size_t)cw * 2 + h) * OT * C2_T;
@@ -513,12 +537,31 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
     }
     const int Qh = tb.Q >> 1;
     c2_tw1_init<true>(tid);
+    const int *cpl = c2_stage_cp(smem, tb, tid);
     __syncthreads();  // the staged statistics
     C2_TP(42);
     for (int m2 = h * Qh; m2 < (h + 1) * Qh; ++m2) {
         const int tl = c2_opaque(tid);
         C2_TPC(32);
         const uint32_t rmk = tb.cmask[tb.Q * C2_T + tl];
+        // the class slice (entries' image positions, beta_prev), requested before the transform and
+        // consumed after it, so its HBM latency hides behind the transform
+        const int q0 = c2_uni(cpl[m2]), q1 = c2_uni(cpl[m2 + 1]);
+        const __amdgpu_buffer_rsrc_t rs = c2_rsrc(s + q0, 4 * (q1 - q0));  // past the class's end: reads 0,
+                                                                           // stores dropped
+        // (at more than 12 outputs per thread the slice stays out of flight during the rows and the
+        // transform: it would spill)
+        constexpr bool EARLY = OT <= 12;
+        float v[C2_SN];
+        uint32_t e[C2_SN];
+        auto load_slice = [&]() {
+            const __amdgpu_buffer_rsrc_t re = c2_rsrc(tb.cls2 + (size_t)m2 * CW2_SLICE, 4 * CW2_SLICE);
+#pragma unroll
+            for (int i = 0; i < C2_SN; ++i) {
+                e[i] = c2_ldu(re, 4 * tl, 4 * i * C2_T);
+                v[i] = c2_ldf(rs, 4 * tl + 4 * i * C2_T, 0);  // (t = 0: unused)
+            }
+        };
         {  // rows r and P - r of each owned pair: sum of al v conj(W) / be v W over its outputs (v = z / phi),
            // branch-free: every slot accumulates (NEWROW restarts the sums) and writes both rows, at the
            // addresses of the host table wab -- the pair's rows on its last slot, the trash slot otherwise
@@ -526,7 +569,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
            // sum.  (a, al, be, v and the addresses reloaded per class from L1 / L2: held across the transform,
            // or loaded one class ahead, they spill; al v and be v precomputed per codeword were slower -- four
            // times the per-codeword bytes re-read from L2 every class.)
-            constexpr int CH = OT > 12 ? (OT + 1) / 2 : OT;  // slots per load round (all of them at 12 per thread)
+            constexpr int CH = OT > 12 ? (OT + 1) / 2 : OT;  // slots per load round (one round at 12 per thread)
             const __amdgpu_buffer_rsrc_t rg = c2_rsrc(tb.gf, 16 * OT * C2_T), rv = c2_rsrc(vz, 4 * OT * C2_T),
                                          rk = c2_rsrc(tb.ka, 4 * OT * C2_T), rw = c2_rsrc(tb.wab, 8 * OT * C2_T);
             cx<float> u0{0.f, 0.f}, u1{0.f, 0.f};
@@ -559,37 +602,33 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
                 }
             }
         }
+        // (requested after the rows' table loads: vector-memory loads complete in order, so a slice
+        // requested before them would hold the rows up for its whole HBM latency)
+        if constexpr (EARLY) load_slice();
+        int sa[2], sb[2];  // the sections' segments of the class (in flight during the transform; sections
+                           // past Lb read 0 as their end: empty)
+        {
+            const __amdgpu_buffer_rsrc_t rg = c2_rsrc(tb.seg + (size_t)m2 * (Lb + 1), 2 * (Lb + 1));
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int sec = tl + k * C2_T;
+                sa[k] = __builtin_amdgcn_raw_buffer_load_b16(rg, 2 * sec, 0, 0);
+                sb[k] = __builtin_amdgcn_raw_buffer_load_b16(rg, 2 * sec + 2, 0, 0);
+            }
+        }
         C2_TPC(33);
         __syncthreads();
         C2_TPC(34);
         c2_fft<true>(tl, rmk);
         C2_TPC(35);
-        const int q0 = c2_uni(tb.cls_ptr[m2]), q1 = c2_uni(tb.cls_ptr[m2 + 1]);
         float snv[C2_SN];
-        const __amdgpu_buffer_rsrc_t rs = c2_rsrc(s + q0, 4 * (q1 - q0));  // past the class's end: reads 0,
-                                                                           // stores dropped
+        if constexpr (!EARLY) load_slice();
         {
-            float v[C2_SN];
-            uint32_t e[C2_SN];
-            const __amdgpu_buffer_rsrc_t re = c2_rsrc(tb.cls2 + (size_t)m2 * CW2_SLICE, 4 * CW2_SLICE);
-#pragma unroll
-            for (int i = 0; i < C2_SN; ++i) {  // every load of the class slice in one round trip
-                e[i] = c2_ldu(re, 4 * tl, 4 * i * C2_T);
-                v[i] = c2_ldf(rs, 4 * tl + 4 * i * C2_T, 0);  // (t = 0: unused)
-            }
 #pragma unroll
             for (int i = 0; i < C2_SN; ++i) {  // s = beta_prev + tau u (sparc.py:972); beta_prev stored by cw2_ab
                 const float b = have_beta ? v[i] : 0.f;
                 snv[i] = b + tau * dr[e[i] & 0xffffu];
             }
-        }
-        int sa[2], sb[2];  // the sections' segments of the class
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int sec = tl + k * C2_T;
-            const uint16_t *sg = tb.seg + (size_t)m2 * (Lb + 1);
-            sa[k] = sec < Lb ? sg[sec] : 0;
-            sb[k] = sec < Lb ? sg[sec + 1] : 0;
         }
         C2_TPC(36);
 #pragma unroll
