@@ -631,9 +631,11 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
             }
         }
         C2_TPC(36);
+#ifndef C2_DIAG_NO_SSTORE  // (diagnostic builds only: timing without the s stores)
 #pragma unroll
         for (int c = 0; c < C2_SN; ++c)  // s to HBM straight from the registers (class order)
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, snv[c]), rs, 4 * tl + 4 * c * C2_T, 0, 0);
+#endif
         C2_TPC(37);
         __syncthreads();
         C2_TPC(38);
