@@ -29,7 +29,7 @@ namespace sg {
 constexpr int B2_THREADS = 1024;
 constexpr int B2_LOG2P = 14, B2_P = 1 << B2_LOG2P;
 constexpr int B2_J = 32;  // column entries per thread (Mc = 32768)
-constexpr int B2_JR = 24;  // of which blk2_ab holds in registers (the other 8 in LDS: 32 KB)
+constexpr int B2_JR = 32;  // of which blk2_ab holds in registers (any rest in the LDS past the image)
 
 namespace {
 

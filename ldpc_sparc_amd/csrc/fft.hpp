@@ -38,11 +38,21 @@ __device__ __forceinline__ cx<T> cmul(cx<T> a, cx<T> b) {
 // needs a wait state that it does not insert for an asm block -- measured
 // wrong in tools/fftbench's accuracy check).
 typedef float sg_f2 __attribute__((ext_vector_type(2)));
+// The packed instructions' modifiers negate whole operands and the compiler
+// does not fold a one-lane negation into them (a {-y, y} operand costs a xor
+// and a move), so the sign patterns are constant pairs (amp_cw2.hip c2_mul).
+__device__ __forceinline__ sg_f2 sg_pm() { return sg_f2{1.f, -1.f}; }
+__device__ __forceinline__ sg_f2 sg_mp() { return sg_f2{-1.f, 1.f}; }
 template <>
 __device__ __forceinline__ cx<float> cmul<float>(cx<float> a, cx<float> b) {
     const sg_f2 A = {a.x, a.y}, B = {b.x, b.y};
-    const sg_f2 an = {-a.y, a.y};
-    const sg_f2 r = __builtin_elementwise_fma(an, B.yx, A.xx * B);
+    const sg_f2 r = __builtin_elementwise_fma(A.yy * B.yx, sg_mp(), A.xx * B);
+    return {r.x, r.y};
+}
+// a conj(b) in three packed instructions
+__device__ __forceinline__ cx<float> cmulc_f(cx<float> a, cx<float> b) {
+    const sg_f2 A = {a.x, a.y}, B = {b.x, b.y};
+    const sg_f2 r = __builtin_elementwise_fma(A.yy, B.yx, (A.xx * B) * sg_pm());
     return {r.x, r.y};
 }
 // x + a b and x + a conj(b) in two packed FMAs (single precision)
@@ -63,7 +73,12 @@ __device__ __forceinline__ cx<T> cconj(cx<T> a) { return {a.x, -a.y}; }
 // multiply by -i (forward) or +i (inverse)
 template <typename T, bool INV>
 __device__ __forceinline__ cx<T> mul_mi(cx<T> a) {
-    return INV ? cx<T>{-a.y, a.x} : cx<T>{a.y, -a.x};
+    if constexpr (sizeof(T) == 4) {
+        const sg_f2 r = sg_f2{a.y, a.x} * (INV ? sg_mp() : sg_pm());
+        return {r.x, r.y};
+    } else {
+        return INV ? cx<T>{-a.y, a.x} : cx<T>{a.y, -a.x};
+    }
 }
 
 template <typename T, bool INV>
@@ -75,12 +90,24 @@ __device__ __forceinline__ void dft2(cx<T> *a) {
 
 template <typename T, bool INV>
 __device__ __forceinline__ void dft4(cx<T> *a) {
-    const cx<T> t0 = cadd(a[0], a[2]), t1 = csub(a[0], a[2]);
-    const cx<T> t2 = cadd(a[1], a[3]), t3 = mul_mi<T, INV>(csub(a[1], a[3]));
-    a[0] = cadd(t0, t2);
-    a[2] = csub(t0, t2);
-    a[1] = cadd(t1, t3);
-    a[3] = csub(t1, t3);
+    if constexpr (sizeof(T) == 4) {  // x -+ i d as one packed FMA with a constant sign pair
+        const sg_f2 a0 = {a[0].x, a[0].y}, a1 = {a[1].x, a[1].y}, a2 = {a[2].x, a[2].y}, a3 = {a[3].x, a[3].y};
+        const sg_f2 t0 = a0 + a2, t1 = a0 - a2, t2 = a1 + a3, d = a1 - a3;
+        const sg_f2 r0 = t0 + t2, r2 = t0 - t2;
+        const sg_f2 r1 = __builtin_elementwise_fma(d.yx, INV ? sg_mp() : sg_pm(), t1);
+        const sg_f2 r3 = __builtin_elementwise_fma(d.yx, INV ? sg_pm() : sg_mp(), t1);
+        a[0] = {r0.x, r0.y};
+        a[1] = {r1.x, r1.y};
+        a[2] = {r2.x, r2.y};
+        a[3] = {r3.x, r3.y};
+    } else {
+        const cx<T> t0 = cadd(a[0], a[2]), t1 = csub(a[0], a[2]);
+        const cx<T> t2 = cadd(a[1], a[3]), t3 = mul_mi<T, INV>(csub(a[1], a[3]));
+        a[0] = cadd(t0, t2);
+        a[2] = csub(t0, t2);
+        a[1] = cadd(t1, t3);
+        a[3] = csub(t1, t3);
+    }
 }
 
 template <typename T, bool INV>
@@ -123,7 +150,13 @@ __device__ __forceinline__ void dft16(cx<T> *a) {
     }
     // y[n2][k1] *= w16^(n2 k1) (forward w16 = e^{-i pi/8}; inverse conjugated)
     auto tw16 = [&](cx<T> x, T c, T s) -> cx<T> {  // x * (c - i s) forward, (c + i s) inverse
-        return INV ? cx<T>{x.x * c - x.y * s, x.x * s + x.y * c} : cx<T>{x.x * c + x.y * s, x.y * c - x.x * s};
+        if constexpr (sizeof(T) == 4) {
+            const sg_f2 X = {x.x, x.y};
+            const sg_f2 r = __builtin_elementwise_fma(X.yx, INV ? sg_f2{-s, s} : sg_f2{s, -s}, X * sg_f2{c, c});
+            return {r.x, r.y};
+        } else {
+            return INV ? cx<T>{x.x * c - x.y * s, x.x * s + x.y * c} : cx<T>{x.x * c + x.y * s, x.y * c - x.x * s};
+        }
     };
     y[1][1] = tw16(y[1][1], c1, s1);
     y[1][2] = tw16(y[1][2], r2, r2);
@@ -288,7 +321,19 @@ __device__ __forceinline__ void tw_expand(const cx<T> *wl, cx<T> *w /* [R], w[0]
 // use (fewer live registers than the expanded w[R]; identical arithmetic)
 template <typename T, bool INV, int R>
 __device__ __forceinline__ void tw_apply(const cx<T> *wl, cx<T> *v) {
-    if constexpr (R == 16) {
+    if constexpr (R == 16 && sizeof(T) == 4) {  // the products of the forward twiddles; the inverse
+                                                // applies their conjugates (three packed instructions)
+        auto ap = [&](cx<float> x, cx<float> w) { return INV ? cmulc_f(x, w) : cmul(x, w); };
+#pragma unroll
+        for (int b = 1; b < 4; ++b) v[b] = ap(v[b], wl[b - 1]);
+#pragma unroll
+        for (int q = 1; q < 4; ++q) {
+            const cx<T> wq = wl[q + 2];  // w^4, w^8, w^12
+            v[4 * q] = ap(v[4 * q], wq);
+#pragma unroll
+            for (int b = 1; b < 4; ++b) v[4 * q + b] = ap(v[4 * q + b], cmul(wq, wl[b - 1]));
+        }
+    } else if constexpr (R == 16) {
         cx<T> a[6];
 #pragma unroll
         for (int t = 0; t < 6; ++t) a[t] = INV ? cconj(wl[t]) : wl[t];
