@@ -276,7 +276,7 @@ int blk_launch_az(const BlkTables &tb, const AmpBufs<float> &bf, bool then_ab,
 int blk_launch_g(const BlkTables &tb, const AmpBufs<float> &bf, cx<float> *gbuf, hipStream_t s);  // G slots
 // two-class form for w = 2^16 (amp_block2.hip)
 int blk2_launch_ab(const BlkTables &tb, const AmpBufs<float> &bf, hipStream_t s);
-int blk2_launch_az(const BlkTables &tb, const AmpBufs<float> &bf, cx<float> *gbuf, hipStream_t s);  // z/phi -> G slots (gbuf [B][ngs]) -> beta, section statistics
+int blk2_launch_az(const BlkTables &tb, const AmpBufs<float> &bf, cx<float> *gbuf, bool then_ab, hipStream_t s);  // z/phi -> G slots (gbuf [B][ngs]) -> beta, section statistics
 int amp_launch_count(const int32_t *map_idx, const int32_t *true_idx, const int32_t *t_final, int B, int L,
                      int logM, int64_t *counts, hipStream_t s);
 

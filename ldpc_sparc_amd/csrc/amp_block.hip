@@ -170,12 +170,39 @@ __device__ __forceinline__ cx<float> bk_gslot(const BlkTables &tb, const AmpBufs
     }
     return acc;
 }
+// One thread per G slot and BK_GCW codewords: the slot's table entries (row,
+// up to four output indices and coefficients: 52 B) are read once for the
+// group instead of once per codeword (with one codeword per thread they were
+// re-read from beyond L2 for every codeword, ~6 MB per codeword at the
+// notebook geometry).
+constexpr int BK_GCW = 16;
 __global__ __launch_bounds__(256) void blk_g(BlkTables tb, AmpBufs<float> bf, cx<float> *gbuf) {
-    const int cw = blockIdx.y;
-    if (!bf.active[cw]) return;
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= tb.ngs) return;
-    gbuf[(size_t)cw * tb.ngs + g] = bk_gslot(tb, bf, cw, g);
+    const int row = tb.grow[g];
+    int gi[4];
+    cx<float> gc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        gi[k] = tb.gi[4 * g + k];
+        gc[k] = tb.gc[4 * g + k];
+    }
+    const int c0 = blockIdx.y * BK_GCW, c1 = min(c0 + BK_GCW, bf.B);
+    for (int cw = c0; cw < c1; ++cw) {
+        if (!bf.active[cw]) continue;
+        const float *z = bf.z + (size_t)cw * tb.n + (size_t)row * tb.Mr;
+        const float phi = (float)bf.phi[(size_t)cw * tb.Lr + row];
+        cx<float> acc{0.f, 0.f};  // same terms, same order as bk_gslot
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (gi[k] >= 0) {
+                const float v = z[gi[k]] / phi;  // Az(z / phi), sparc.py:972
+                acc.x += gc[k].x * v;
+                acc.y += gc[k].y * v;
+            }
+        }
+        gbuf[(size_t)cw * tb.ngs + g] = acc;
+    }
 }
 
 // ------------------------------------------------------------------ Az + eta
@@ -332,7 +359,7 @@ static void bk_launch_az(const BlkTables &tb, const AmpBufs<float> &bf, int do_a
 int blk_launch_g(const BlkTables &tb, const AmpBufs<float> &bf, cx<float> *gbuf, hipStream_t s) {
     if (bf.B <= 0) return SG_OK;
     ProfScope ps(SG_PH_AZ_A, s);
-    hipLaunchKernelGGL(blk_g, dim3((tb.ngs + 255) / 256, bf.B), dim3(256), 0, s, tb, bf, gbuf);
+    hipLaunchKernelGGL(blk_g, dim3((tb.ngs + 255) / 256, (bf.B + BK_GCW - 1) / BK_GCW), dim3(256), 0, s, tb, bf, gbuf);
     SG_HIP(hipGetLastError());
     return SG_OK;
 }

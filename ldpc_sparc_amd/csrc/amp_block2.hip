@@ -102,25 +102,14 @@ __device__ __forceinline__ void b2_fwd_stages(cx<float> *d, const cx<float> *__r
 size_t blk2_lds_bytes() { return (size_t)B2_P * sizeof(cx<float>) + (size_t)(B2_J - B2_JR) * B2_THREADS * 4; }
 
 // ------------------------------------------------------------------ Ab
-template <int EPS>
-__global__ __launch_bounds__(B2_THREADS) void blk2_ab(BlkTables tb, AmpBufs<float> bf) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+// The column's forward transforms from beta_c in registers (bv[i] = beta_c at
+// b2_j(tid, i)): for each transform and class, scatter -> three radix-16
+// stages -> the needed outputs (last radix-4 stage and class factor folded into
+// the coefficients), summed over the classes in registers -> rbuf[t]
+__device__ __forceinline__ void b2_ab_column(const BlkTables &tb, const AmpBufs<float> &bf, int c, int cw, int tid,
+                                             const float *bv, unsigned char *smem) {
     cx<float> *d = reinterpret_cast<cx<float> *>(smem);
     float *dr = reinterpret_cast<float *>(smem);
-    const int c = blockIdx.x, cw = blockIdx.y, tid = threadIdx.x;
-    if (!bf.active[cw]) return;
-    const float *beta = bf.beta + (size_t)cw * tb.LM + (size_t)c * tb.Mc;
-    // beta_c read once for all the column's transforms and classes: entries
-    // 0..B2_JR-1 of the thread in registers, the rest in the LDS past the image
-    // (all in registers spills around the transform)
-    float bv[B2_JR];
-    float *bx = reinterpret_cast<float *>(smem + (size_t)B2_P * sizeof(cx<float>));
-#pragma unroll
-    for (int i = 0; i < B2_J; ++i) {
-        const float b = beta[b2_j<EPS>(tid, i)];
-        if (i < B2_JR) bv[i < B2_JR ? i : 0] = b;
-        else bx[(i - B2_JR) * B2_THREADS + tid] = b;
-    }
     for (int q = tb.col_ptr[c]; q < tb.col_ptr[c + 1]; ++q) {
         const int t = tb.col_t[q];
         float acc = 0.f;  // output tid (Mr <= 1024), summed over the two classes
@@ -134,8 +123,7 @@ __global__ __launch_bounds__(B2_THREADS) void blk2_ab(BlkTables tb, AmpBufs<floa
 #pragma unroll
             for (int i = 0; i < B2_J; ++i) {
                 const uint32_t p = b2_pos(pv, i);
-                const float b = i < B2_JR ? bv[i < B2_JR ? i : 0] : bx[(i - B2_JR) * B2_THREADS + tl];
-                if ((int)(p >> 15) == m2) dr[p & 0x7fffu] = b;
+                if ((int)(p >> 15) == m2) dr[p & 0x7fffu] = bv[i];
             }
             __syncthreads();
             b2_fwd_stages(d, tb.stw, tl);
@@ -158,9 +146,24 @@ __global__ __launch_bounds__(B2_THREADS) void blk2_ab(BlkTables tb, AmpBufs<floa
     }
 }
 
+// Standalone Ab (beta_c read once for all the column's transforms and
+// classes); iterations after the first run it inside the previous blk2_az
+template <int EPS>
+__global__ __launch_bounds__(B2_THREADS) void blk2_ab(BlkTables tb, AmpBufs<float> bf) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int c = blockIdx.x, cw = blockIdx.y, tid = threadIdx.x;
+    if (!bf.active[cw]) return;
+    const float *beta = bf.beta + (size_t)cw * tb.LM + (size_t)c * tb.Mc;
+    float bv[B2_J];
+#pragma unroll
+    for (int i = 0; i < B2_J; ++i) bv[i] = beta[b2_j<EPS>(tid, i)];
+    b2_ab_column(tb, bf, c, cw, tid, bv, smem);
+}
+
 // ------------------------------------------------------------------ Az + eta
 template <int EPS>
-__global__ __launch_bounds__(B2_THREADS) void blk2_az(BlkTables tb, AmpBufs<float> bf, const cx<float> *gbuf) {
+__global__ __launch_bounds__(B2_THREADS) void blk2_az(BlkTables tb, AmpBufs<float> bf, const cx<float> *gbuf,
+                                                      int do_ab) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     cx<float> *d = reinterpret_cast<cx<float> *>(smem);
     float *dr = reinterpret_cast<float *>(smem);
@@ -215,6 +218,7 @@ __global__ __launch_bounds__(B2_THREADS) void blk2_az(BlkTables tb, AmpBufs<floa
     const float tau = (float)bf.tau[(size_t)cw * tb.Lc + c];
     float *beta = bf.beta + (size_t)cw * tb.LM + (size_t)c * tb.Mc;
     const int l0 = c * nsec;  // first section of the column block
+    float bv[B2_J];  // the new beta_c, kept for the next iteration's Ab (do_ab)
 #pragma unroll
     for (int sq = 0; sq < spw; ++sq) {
         const int ls = wv * spw + sq;  // section within the column block
@@ -251,6 +255,7 @@ __global__ __launch_bounds__(B2_THREADS) void blk2_az(BlkTables tb, AmpBufs<floa
         for (int e = 0; e < eps; ++e) {
             const float b = x[e] / dn;
             beta[ls * tb.M + lane * eps + e] = b;
+            bv[i0 + e] = b;
             const float dl = b - ((lane * eps + e) == truth ? 1.f : 0.f);
             ss += b * b;
             se += dl * dl;
@@ -263,6 +268,13 @@ __global__ __launch_bounds__(B2_THREADS) void blk2_az(BlkTables tb, AmpBufs<floa
             bf.sec_err[o] = (double)se;
             bf.sec_argmax[o] = arg;
         }
+    }
+    // the next iteration's forward transforms of the column from the new beta_c
+    // in registers (not read back; a codeword that stops in this iteration
+    // computes one Ab nobody reads)
+    if (do_ab) {
+        __syncthreads();  // the image is free
+        b2_ab_column(tb, bf, c, cw, tid, bv, smem);
     }
 }
 
@@ -294,10 +306,11 @@ static void b2_launch_ab(const BlkTables &tb, const AmpBufs<float> &bf, size_t l
     if (*rc == SG_OK) hipLaunchKernelGGL(blk2_ab<EPS>, dim3(tb.Lc, bf.B), dim3(B2_THREADS), lds, s, tb, bf);
 }
 template <int EPS>
-static void b2_launch_az(const BlkTables &tb, const AmpBufs<float> &bf, const cx<float> *gbuf, size_t lds,
+static void b2_launch_az(const BlkTables &tb, const AmpBufs<float> &bf, const cx<float> *gbuf, int do_ab, size_t lds,
                          hipStream_t s, int *rc) {
     *rc = blk2_set_attrs<EPS>(lds);
-    if (*rc == SG_OK) hipLaunchKernelGGL(blk2_az<EPS>, dim3(tb.Lc, bf.B), dim3(B2_THREADS), lds, s, tb, bf, gbuf);
+    if (*rc == SG_OK)
+        hipLaunchKernelGGL(blk2_az<EPS>, dim3(tb.Lc, bf.B), dim3(B2_THREADS), lds, s, tb, bf, gbuf, do_ab);
 }
 
 int blk2_launch_ab(const BlkTables &tb, const AmpBufs<float> &bf, hipStream_t s) {
@@ -313,14 +326,14 @@ int blk2_launch_ab(const BlkTables &tb, const AmpBufs<float> &bf, hipStream_t s)
     return SG_OK;
 }
 
-int blk2_launch_az(const BlkTables &tb, const AmpBufs<float> &bf, cx<float> *gbuf, hipStream_t s) {
+int blk2_launch_az(const BlkTables &tb, const AmpBufs<float> &bf, cx<float> *gbuf, bool then_ab, hipStream_t s) {
     if (bf.B <= 0) return SG_OK;
     if (tb.Mc != 2 * B2_P) return fail(SG_ERR_UNSUPPORTED, "block engine (two classes): Mc=%d", tb.Mc);
     SG_TRY(blk_launch_g(tb, bf, gbuf, s));
     const size_t lds = blk2_lds_bytes();
     int rc = SG_OK;
     ProfScope ps(SG_PH_AZ_B, s);
-    B2_EPS_DISPATCH(tb.M, b2_launch_az, tb, bf, (const cx<float> *)gbuf, lds, s, &rc);
+    B2_EPS_DISPATCH(tb.M, b2_launch_az, tb, bf, (const cx<float> *)gbuf, then_ab ? 1 : 0, lds, s, &rc);
     SG_TRY(rc);
     SG_HIP(hipGetLastError());
     return SG_OK;

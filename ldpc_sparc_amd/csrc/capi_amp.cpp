@@ -1398,10 +1398,9 @@ static int decode_impl(sg_amp_plan *p, const void *d_y, int B, const int32_t *d_
     for (int t = 0; t < t_max - 1; ++t) {
         if constexpr (sizeof(T) == 4) {
             if (blk) {
-                // (the single-class block engine runs iteration t's Ab inside iteration t - 1's Az)
-                if (t > 0 && p->block2) SG_TRY(blk2_launch_ab(bt, bf, s));
+                // (both block engines run iteration t's Ab inside iteration t - 1's Az)
                 SG_TRY(amp_launch_control<T>(tb, bf, sc, pr, 0, t, s));
-                SG_TRY(p->block2 ? blk2_launch_az(bt, bf, (cx<float> *)p->ws_gbuf, s)
+                SG_TRY(p->block2 ? blk2_launch_az(bt, bf, (cx<float> *)p->ws_gbuf, t + 1 < t_max - 1, s)
                                  : blk_launch_az(bt, bf, t + 1 < t_max - 1, s));
                 SG_TRY(amp_launch_control<T>(tb, bf, sc, pr, 1, t, s));
             }
