@@ -770,10 +770,16 @@ def main():
         procs = cpu_pool.host_cores()
 
     st = amp_setup(args, d.rank)
-    for _ in range(args.warmup):
+    # per-kernel breakdown from the last warmup step; the timed steps bracket each AMP iteration only
+    # (level 2: an event record between two kernels holds the second back by several microseconds)
+    fine = {}
+    for i in range(args.warmup):
+        pf = _native.Profiler() if i == args.warmup - 1 else None
         amp_step(st, args, comm)
+        if pf is not None:
+            fine = pf.stop()
     _native.device_synchronize()
-    prof = _native.Profiler()
+    prof = _native.Profiler(level=2 if args.warmup > 0 else 1)
     d.barrier()
     _native.device_synchronize()
     t0 = time.perf_counter()
@@ -795,7 +801,7 @@ def main():
     # the engine this batch ran on (2: per-codeword amp_cw.hip, 1: staged amp_fused.hip)
     engine = _native.lib().sg_amp_plan_engine(st["plan"], st["B"])
     last = _native.amp_last_decode(st["plan"])
-    split = phases.get("cw2_az", (0.0, 0))[1] > 0
+    split = max(phases.get("cw2_az", (0.0, 0))[1], fine.get("cw2_az", (0.0, 0))[1]) > 0
     engine_name = {1: "staged (amp_fused.hip)",
                    2: ("split per-codeword (amp_cw2.hip)" if split else "per-codeword (amp_cw.hip)")}.get(
         engine, str(engine))
@@ -843,9 +849,13 @@ def main():
                      "codeword_iterations": cw_it, "codeword_iterations_per_launch": cw_it_per_launch,
                      "kernel_ms": {k: round(v[0], 3) for k, v in phases.items()},
                      "launches": {k: v[1] for k, v in phases.items()},
+                     "kernel_ms_last_warmup_step": {k: round(v[0], 3) for k, v in fine.items()},
+                     "launches_last_warmup_step": {k: v[1] for k, v in fine.items()},
                      "note": "binding bound: SURVEY.md 8(d) flops (2 transforms x 2.5 w log2 w + 20 L M) at the "
                              "f32 vector peak (the FFTs run on the VALU); achieved = flops x executed codeword-"
-                             "iterations / summed kernel time (HIP events on the library stream)"},
+                             "iterations / summed kernel time (HIP events on the library stream around every AMP "
+                             "iteration of the timed steps; the per-kernel split is from the last warmup step, "
+                             "whose events also sit between the kernels)"},
         "roofline_hbm": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": gbs / HBM_PEAK_GBS if gbs else None,
                          "algorithmic_bytes_per_codeword_iteration": bytes_per_cwit,

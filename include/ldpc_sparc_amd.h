@@ -69,7 +69,12 @@ int sg_device_synchronize(void);
 /* Per-phase kernel timing.  When enabled, every kernel launch of the decoders
  * is bracketed by HIP events on the stream it is launched on; collect
  * synchronises the pending events, returns the summed milliseconds and the
- * launch count per phase (arrays of SG_PH_COUNT) and resets the counters. */
+ * launch count per phase (arrays of SG_PH_COUNT) and resets the counters.
+ * on = 2 records only the per-iteration scope of the split per-codeword
+ * engine, not its per-kernel scopes inside it: every timed event record on a
+ * stream holds the next kernel back by several microseconds, so bench.py's
+ * timed region brackets each iteration (two events) rather than each of its
+ * four kernels. */
 enum sg_phase {
     SG_PH_AB_A = 0, SG_PH_AB_B = 1, SG_PH_AZ_A = 2, SG_PH_AZ_B = 3, SG_PH_ETA = 4,
     SG_PH_CONTROL = 5, SG_PH_BP = 6, SG_PH_DENSE = 7, SG_PH_AMP_CW = 8, SG_PH_CW2_AB = 9, SG_PH_CW2_AZ = 10,

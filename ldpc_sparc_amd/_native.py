@@ -271,10 +271,11 @@ def device_synchronize():
 
 class Profiler:
     """Per-phase kernel timing through HIP events on the launch streams
-    (sg_profile_enable / sg_profile_collect)."""
+    (sg_profile_enable / sg_profile_collect).  level 2: the split engine's
+    per-iteration scope only, without events between its kernels."""
 
-    def __init__(self):
-        check(lib().sg_profile_enable(1))
+    def __init__(self, level=1):
+        check(lib().sg_profile_enable(level))
         self.collect()  # drop anything recorded before
 
     def collect(self):

@@ -44,7 +44,8 @@ struct BlkTables {
     int nT, L, M, LM, n, Lr, Lc, Mr, Mc;
     const int32_t *col_ptr, *col_t, *t_row;
     const uint32_t *pos2;     // [nT][8][1024] real LDS index (2 fsw(m) + component) of column entry
-                              // j = tid + 1024 i, pairs (i = 2 i2, 2 i2 + 1) at [t][i2][tid]
+                              // j = tid + 1024 i, pairs (i = 2 i2, 2 i2 + 1) at [t][i2][tid]; the two-class
+                              // engine: [nT][2][16][1024], 2 ppos(m1) + component per class (amp_block2.hip)
     const uint32_t *oab;      // [nT][Mr] (a mod 4096) | (b mod 4096) << 16 of output i
     const cx<float> *oc;      // [nT][Mr][8] X_i = Re(sum_r al_r Y[a mod 4096 + 4096 r] + be_r conj Y[b mod ...]),
                               // al_r = c1 w_N2^(r a), be_r = c2 conj w_N2^(r b) (the last FFT stage folded in)
@@ -218,7 +219,7 @@ struct Cw2Tables {
     const uint32_t *cls2;     // [Q][9216] cls_ls of each class padded to 9216 entries with CW2_TRASH
     const int32_t *qpos;      // [Mc]
     const uint16_t *seg;      // [Q][Lblk+1]
-    float4 *xp;               // [B][2][OT][512] partial (H[a], conj H[b]) of each half
+    float *xr;                // [B][2][OT][512] each half's part of Re(c1 H[a] + c2 conj H[b]) per output
     const uint2 *rab;         // [OT][512] LDS byte addresses of rows r, P - r of the slot's output (cw2_ab reads)
     const uint2 *wab;         // [OT][512] LDS byte addresses of the slot's row writes (rows r, P - r on the
                               // pair's last slot, else the trash slot; r = 0, P / 2: row r and trash)

@@ -156,13 +156,13 @@ __device__ __forceinline__ void bk_ab_column(const BlkTables &tb, const AmpBufs<
 __device__ __forceinline__ cx<float> bk_gslot(const BlkTables &tb, const AmpBufs<float> &bf, int cw, int g) {
     const int row = tb.grow[g];
     const float *z = bf.z + (size_t)cw * tb.n + (size_t)row * tb.Mr;
-    const float phi = (float)bf.phi[(size_t)cw * tb.Lr + row];
+    const float iphi = 1.0f / (float)bf.phi[(size_t)cw * tb.Lr + row];
     cx<float> acc{0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int i = tb.gi[4 * g + k];
         if (i >= 0) {
-            const float v = z[i] / phi;  // Az(z / phi), sparc.py:972
+            const float v = z[i] * iphi;  // Az(z / phi), sparc.py:972 (one division per slot)
             const cx<float> cc = tb.gc[4 * g + k];
             acc.x += cc.x * v;
             acc.y += cc.y * v;
@@ -191,12 +191,12 @@ __global__ __launch_bounds__(256) void blk_g(BlkTables tb, AmpBufs<float> bf, cx
     for (int cw = c0; cw < c1; ++cw) {
         if (!bf.active[cw]) continue;
         const float *z = bf.z + (size_t)cw * tb.n + (size_t)row * tb.Mr;
-        const float phi = (float)bf.phi[(size_t)cw * tb.Lr + row];
+        const float iphi = 1.0f / (float)bf.phi[(size_t)cw * tb.Lr + row];
         cx<float> acc{0.f, 0.f};  // same terms, same order as bk_gslot
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             if (gi[k] >= 0) {
-                const float v = z[gi[k]] / phi;  // Az(z / phi), sparc.py:972
+                const float v = z[gi[k]] * iphi;  // Az(z / phi), sparc.py:972
                 acc.x += gc[k].x * v;
                 acc.y += gc[k].y * v;
             }
@@ -267,14 +267,14 @@ __global__ __launch_bounds__(BK_THREADS) void blk_az(BlkTables tb, AmpBufs<float
     const int lane = tid & 63, wv = tid >> 6;
     constexpr int eps = EPS, spw = 1024 / (64 * EPS);
     const int nsec = tb.Mc / tb.M;
-    const float tau = (float)bf.tau[(size_t)cw * tb.Lc + c];
+    const float tau = (float)bf.tau[(size_t)cw * tb.Lc + c], itau = 1.0f / tau;
     float *beta = bf.beta + (size_t)cw * tb.LM + (size_t)c * tb.Mc;
     float s[BK_J], x[BK_J], bv[BK_J];
 #pragma unroll
     for (int i = 0; i < BK_J; ++i) {
         const int j = bk_j<EPS>(tid, i);
         s[i] = beta[j] + tau * u[i];  // sparc.py:972
-        x[i] = s[i] / tau;            // sparc.py:430
+        x[i] = s[i] * itau;           // sparc.py:430 (reciprocal once: IEEE division is ~10 VALU)
     }
     const int l0 = c * nsec;  // first section of the column block
 #pragma unroll
@@ -302,11 +302,12 @@ __global__ __launch_bounds__(BK_THREADS) void blk_az(BlkTables tb, AmpBufs<float
             dn += x[i0 + e];
         }
         dn = bk_wave_sum(dn);
+        const float idn = 1.0f / dn;
         const int truth = bf.true_idx ? bf.true_idx[(size_t)cw * tb.L + l0 + ls] : -1;
         float ss = 0.f, se = 0.f;
 #pragma unroll
         for (int e = 0; e < eps; ++e) {
-            const float b = x[i0 + e] / dn;
+            const float b = x[i0 + e] * idn;
             beta[ls * tb.M + lane * eps + e] = b;
             bv[i0 + e] = b;
             const float dl = b - ((lane * eps + e) == truth ? 1.f : 0.f);

@@ -30,6 +30,13 @@ constexpr int B2_THREADS = 1024;
 constexpr int B2_LOG2P = 14, B2_P = 1 << B2_LOG2P;
 constexpr int B2_J = 32;  // column entries per thread (Mc = 32768)
 constexpr int B2_JR = 32;  // of which blk2_ab holds in registers (any rest in the LDS past the image)
+// The class image in the padded layout of fft.hpp ppos (element i at i + i/32:
+// every FFT stage access is a per-thread base plus a constant, no swizzle
+// arithmetic); a padding slot -- never written by the rows or the FFT stages,
+// so zero after b2_clear -- is the trash slot of the position tables.
+constexpr int B2_IMG = ppos(B2_P);       // complex slots of the padded image
+constexpr int B2_TRASH = 2 * 32;         // real index of the padding slot at complex position 32
+static_assert(ppos(B2_TRASH / 2) == B2_TRASH / 2 + 1, "the trash slot is a padding slot (capi_amp.cpp build_block2)");
 
 namespace {
 
@@ -57,9 +64,10 @@ __device__ __forceinline__ int b2_opaque(int v) {
 }
 
 __device__ __forceinline__ void b2_clear(unsigned char *smem, int tid) {
+    constexpr int N16 = B2_IMG * (int)sizeof(cx<float>) / 16;  // (8448: 8 per thread and a quarter)
 #pragma unroll
-    for (int i = 0; i < B2_P * (int)sizeof(cx<float>) / 16 / B2_THREADS; ++i)
-        reinterpret_cast<uint4 *>(smem)[tid + i * B2_THREADS] = uint4{0, 0, 0, 0};
+    for (int i = 0; i < (N16 + B2_THREADS - 1) / B2_THREADS; ++i)
+        if (tid + i * B2_THREADS < N16) reinterpret_cast<uint4 *>(smem)[tid + i * B2_THREADS] = uint4{0, 0, 0, 0};
 }
 
 // Column entry i (< 32) of thread tid: wavefront w owns sections
@@ -73,33 +81,26 @@ __device__ __forceinline__ int b2_j(int tid, int i) {
     return ((tid >> 6) * SPW + sq) * M + (tid & 63) * EPS + e;
 }
 
-// class bit (15) | real LDS index in the class image (2 fsw(m1) + component)
-// of the thread's column entries of transform t, packed in pairs
-__device__ __forceinline__ void b2_pos_load(const BlkTables &tb, int t, int tid, uint32_t *pv) {
-    const uint32_t *p2 = tb.pos2 + (size_t)t * (B2_J / 2) * B2_THREADS;
+// real LDS index in the image of class m2 (2 ppos(m1) + component; B2_TRASH
+// for the entries of the other class) of the thread's column entries of
+// transform t, packed in pairs
+__device__ __forceinline__ void b2_pos_load(const BlkTables &tb, int t, int m2, int tid, uint32_t *pv) {
+    const uint32_t *p2 = tb.pos2 + ((size_t)t * 2 + m2) * (B2_J / 2) * B2_THREADS;
 #pragma unroll
     for (int i = 0; i < B2_J / 2; ++i) pv[i] = p2[i * B2_THREADS + tid];
 }
 __device__ __forceinline__ uint32_t b2_pos(const uint32_t *pv, int i) { return (pv[i >> 1] >> (16 * (i & 1))) & 0xffffu; }
 
-// the first three stages (radix 16) of the P-point FFT, as amp_block.hip
-__device__ __forceinline__ void b2_fwd_stages(cx<float> *d, const cx<float> *__restrict__ stw, int tid) {
-    if constexpr (true) {  // sine / cosine twiddles: no table entries in flight (blk2_ab holds beta_c in
-                           // registers; with the table prefetch it spills)
-        lds_fft1_sincos<false, 16, B2_LOG2P, 0, 3>(d, tid);
-    } else {
-        cx<float> w0[1], w1[6], w2[6];
-        fft1_tw_load_ct<float, 16, B2_LOG2P, 1>(stw, tid, w1);
-        stockham1_stage_ct<float, false, 16, 16, B2_LOG2P, 0>(d, w0, tid);
-        fft1_tw_load_ct<float, 16, B2_LOG2P, 2>(stw, tid, w2);
-        stockham1_stage_ct<float, false, 16, 16, B2_LOG2P, 4>(d, w1, tid);
-        stockham1_stage_ct<float, false, 16, 16, B2_LOG2P, 8>(d, w2, tid);
-    }
+// the first three stages (radix 16) of the P-point FFT over the padded image,
+// twiddles from the hardware sine / cosine (no table entries in flight: blk2_ab
+// holds beta_c in registers; with the table prefetch it spills)
+__device__ __forceinline__ void b2_fwd_stages(cx<float> *d, int tid) {
+    lds_fft1_sincos<false, 16, B2_LOG2P, 0, 3, true>(d, tid);
 }
 
 }  // namespace
 
-size_t blk2_lds_bytes() { return (size_t)B2_P * sizeof(cx<float>) + (size_t)(B2_J - B2_JR) * B2_THREADS * 4; }
+size_t blk2_lds_bytes() { return (size_t)B2_IMG * sizeof(cx<float>) + (size_t)(B2_J - B2_JR) * B2_THREADS * 4; }
 
 // ------------------------------------------------------------------ Ab
 // The column's forward transforms from beta_c in registers (bv[i] = beta_c at
@@ -117,16 +118,13 @@ __device__ __forceinline__ void b2_ab_column(const BlkTables &tb, const AmpBufs<
             const int tl = b2_opaque(tid);
             // the positions, in flight while the image clears
             uint32_t pv[B2_J / 2];
-            b2_pos_load(tb, t, tl, pv);
+            b2_pos_load(tb, t, m2, tl, pv);
             b2_clear(smem, tl);
             __syncthreads();
 #pragma unroll
-            for (int i = 0; i < B2_J; ++i) {
-                const uint32_t p = b2_pos(pv, i);
-                if ((int)(p >> 15) == m2) dr[p & 0x7fffu] = bv[i];
-            }
+            for (int i = 0; i < B2_J; ++i) dr[b2_pos(pv, i)] = bv[i];  // (the other class's entries: trash slot)
             __syncthreads();
-            b2_fwd_stages(d, tb.stw, tl);
+            b2_fwd_stages(d, tl);
             // X_i += Re(sum_r al_r Y[a mod 4096 + 4096 r] + be_r conj Y[b mod ...]):
             // the radix-4 stage and w_N2^(m2 k) are in the coefficients
             if (tl < tb.Mr) {
@@ -134,8 +132,8 @@ __device__ __forceinline__ void b2_ab_column(const BlkTables &tb, const AmpBufs<
                 const int ja = ab & 0xffffu, jb = ab >> 16;
                 const cx<float> *oc = tb.oc + (((size_t)t * 2 + m2) * tb.Mr + tl) * 8;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const cx<float> ya = d[fsw(ja + 4096 * r)], yb = d[fsw(jb + 4096 * r)];
+                for (int r = 0; r < 4; ++r) {  // ppos(j + 4096 r) = ppos(j) + 4224 r for j < 4096
+                    const cx<float> ya = d[ppos(ja) + 4224 * r], yb = d[ppos(jb) + 4224 * r];
                     const cx<float> al = oc[r], be = oc[4 + r];
                     acc += (al.x * ya.x - al.y * ya.y) + (be.x * yb.x + be.y * yb.y);
                 }
@@ -192,20 +190,18 @@ __global__ __launch_bounds__(B2_THREADS) void blk2_az(BlkTables tb, AmpBufs<floa
                     const float cs = __builtin_amdgcn_cosf(x), sn = __builtin_amdgcn_sinf(x);
                     v = {v.x * cs - v.y * sn, v.x * sn + v.y * cs};
                 }
-                cx<float> *dst = &d[fsw(k & (B2_P - 1))];
+                cx<float> *dst = &d[ppos(k & (B2_P - 1))];
                 atomicAdd(&dst->x, v.x);
                 atomicAdd(&dst->y, v.y);
             }
             __syncthreads();
-            if constexpr (SG_BLK_SINCOS & 2) lds_fft1_sincos<true, 16, B2_LOG2P, 0, 4>(d, tl);
-            else lds_fft1_ct_lean<float, true, 16, B2_LOG2P>(d, tb.stw, tl);  // no twiddles in flight: u[] stays in registers
+            // (stage twiddles from the hardware sine / cosine: no table entries in flight, u[] stays in registers)
+            lds_fft1_sincos<true, 16, B2_LOG2P, 0, 4, true>(d, tl);
             uint32_t pv[B2_J / 2];
-            b2_pos_load(tb, t, tl, pv);
+            b2_pos_load(tb, t, m2, tl, pv);
 #pragma unroll
-            for (int i = 0; i < B2_J; ++i) {
-                const uint32_t p = b2_pos(pv, i);
-                if ((int)(p >> 15) == m2) u[i] += dr[p & 0x7fffu];
-            }
+            for (int i = 0; i < B2_J; ++i) u[i] += dr[b2_pos(pv, i)];  // (the other class's entries read the
+                                                                      // zero trash slot)
             __syncthreads();
         }
     }
@@ -215,7 +211,7 @@ __global__ __launch_bounds__(B2_THREADS) void blk2_az(BlkTables tb, AmpBufs<floa
     const int lane = tid & 63, wv = tid >> 6;
     constexpr int eps = EPS, spw = 2048 / (64 * EPS);
     const int nsec = tb.Mc / tb.M;
-    const float tau = (float)bf.tau[(size_t)cw * tb.Lc + c];
+    const float tau = (float)bf.tau[(size_t)cw * tb.Lc + c], itau = 1.0f / tau;
     float *beta = bf.beta + (size_t)cw * tb.LM + (size_t)c * tb.Mc;
     const int l0 = c * nsec;  // first section of the column block
     float bv[B2_J];  // the new beta_c, kept for the next iteration's Ab (do_ab)
@@ -227,7 +223,7 @@ __global__ __launch_bounds__(B2_THREADS) void blk2_az(BlkTables tb, AmpBufs<floa
 #pragma unroll
         for (int e = 0; e < eps; ++e) {
             s[e] = beta[ls * tb.M + lane * eps + e] + tau * u[i0 + e];  // sparc.py:972
-            x[e] = s[e] / tau;                                          // sparc.py:430
+            x[e] = s[e] * itau;                                         // sparc.py:430
         }
         float xm = -INFINITY, sm = -INFINITY;
         int arg = 0x7fffffff;
@@ -249,11 +245,12 @@ __global__ __launch_bounds__(B2_THREADS) void blk2_az(BlkTables tb, AmpBufs<floa
             dn += x[e];
         }
         dn = b2_wave_sum(dn);
+        const float idn = 1.0f / dn;
         const int truth = bf.true_idx ? bf.true_idx[(size_t)cw * tb.L + l0 + ls] : -1;
         float ss = 0.f, se = 0.f;
 #pragma unroll
         for (int e = 0; e < eps; ++e) {
-            const float b = x[e] / dn;
+            const float b = x[e] * idn;
             beta[ls * tb.M + lane * eps + e] = b;
             bv[i0 + e] = b;
             const float dl = b - ((lane * eps + e) == truth ? 1.f : 0.f);

@@ -7,8 +7,9 @@
 //             FFT -> for every output i owned by the thread:
 //                 H[a]      += W Y_m2[r],
 //                 conj H[b] += W conj Y_m2[P - r],   W = w_N2^(m2 a), r = a mod P
-//             in registers; the two halves' partials go to xp.
-//   cw2_ctrl  (B)  z = y - Re(c1 H[a] + c2 conj H[b]) + b z, phi, tau
+//             in registers; each half's part of Re(c1 H[a] + c2 conj H[b])
+//             goes to xr.
+//   cw2_ctrl  (B)  z = y - (sum of the halves' parts) + b z, phi, tau
 //             (sparc.py:931-969); z / phi in slot order (vz).
 //   cw2_az    (2 B)  half h of the classes: rows r and P - r of each owned
 //             conjugate pair from the outputs' al z/phi conj(W) and be z/phi W
@@ -418,9 +419,14 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
         accumulate((h + 1) * Qh - 1, ka);
     }
     C2_TP(11);
-    float4 *xp = tb.xp + ((size_t)cw * 2 + h) * OT * C2_T;
+    // this half's part of the forward output Re(c1 H[a] + c2 conj H[b]) (linear in H: cw2_ctrl adds the
+    // two halves' parts; a quarter of the bytes of the partial H pair)
+    float *xr = tb.xr + ((size_t)cw * 2 + h) * OT * C2_T;
 #pragma unroll
-    for (int j = 0; j < OT; ++j) xp[j * C2_T + tid] = make_float4(Ha[j].x, Ha[j].y, Hb[j].x, Hb[j].y);
+    for (int j = 0; j < OT; ++j) {
+        const float4 c = tb.cf[j * C2_T + tid];
+        xr[j * C2_T + tid] = (c.x * Ha[j].x - c.y * Ha[j].y) + (c.z * Hb[j].x - c.w * Hb[j].y);
+    }
 }
 
 // ---------------------------------------------------------------------------- control
@@ -463,7 +469,7 @@ __global__ __launch_bounds__(C2_T) void cw2_ctrl(Cw2Tables tb, RegBufs<float> bf
         g = pr.W[0];
         if (tid == 0) sc.gamma[cw] = g;
     }
-    const float4 *xp0 = tb.xp + (size_t)cw * 2 * OT * C2_T, *xp1 = xp0 + (size_t)OT * C2_T;
+    const float *xr0 = tb.xr + (size_t)cw * 2 * OT * C2_T, *xr1 = xr0 + (size_t)OT * C2_T;
     float zr[OT];
     double acc = 0.0;
     {
@@ -479,11 +485,7 @@ __global__ __launch_bounds__(C2_T) void cw2_ctrl(Cw2Tables tb, RegBufs<float> bf
         for (int j = 0; j < OT; ++j) {
             float zn = yv[j];
             if (have_beta) {  // Onsager residual, sparc.py:943-946
-                const float4 x0 = xp0[j * C2_T + tid], x1 = xp1[j * C2_T + tid];
-                const float4 c = tb.cf[j * C2_T + tid];
-                const cx<float> ha = {x0.x + x1.x, x0.y + x1.y}, hb = {x0.z + x1.z, x0.w + x1.w};
-                float r = 0.f;
-                r += (c.x * ha.x - c.y * ha.y) + (c.z * hb.x - c.w * hb.y);  // Re(c1 H[a] + c2 conj H[b])
+                const float r = xr0[j * C2_T + tid] + xr1[j * C2_T + tid];  // Re(c1 H[a] + c2 conj H[b])
                 zn = (yv[j] - r) + bco * zv[j];
             }
             zr[j] = zn;
@@ -507,10 +509,10 @@ __global__ __launch_bounds__(C2_T) void cw2_ctrl(Cw2Tables tb, RegBufs<float> bf
         bf.phi[cw] = phi;
         bf.tau[cw] = tv_new;
     }
-    const float phf = (float)phi;
+    const float iph = (float)(1.0 / phi);
     float *vz = tb.vz + (size_t)cw * OT * C2_T;
 #pragma unroll
-    for (int j = 0; j < OT; ++j) vz[j * C2_T + tid] = zr[j] / phf;  // z / phi (sparc.py:972)
+    for (int j = 0; j < OT; ++j) vz[j * C2_T + tid] = zr[j] * iph;  // z / phi (sparc.py:972)
 }
 
 // ---------------------------------------------------------------------------- Az

@@ -56,6 +56,10 @@ struct sg_amp_plan {
          *r_twb = nullptr;
     uint64_t *tprof = nullptr;  // diagnostics: stage-1 phase timestamps (SG_AMP_TPROF)
     size_t tprof_items = 0;
+    // active-flag poll (ActivePoll): pinned host copy and its completion event
+    int32_t *h_active = nullptr;
+    int h_active_cap = 0;
+    hipEvent_t poll_ev = nullptr;
     void *ws_s = nullptr, *ws_tu = nullptr, *ws_xn = nullptr, *ws_part = nullptr, *ws_stM = nullptr,
          *ws_stI = nullptr;
     double *ws_tau_prev = nullptr;
@@ -214,7 +218,7 @@ static int ensure_ws(sg_amp_plan *p, int B, int t_max) {
             SG_HIP(hipMemset(p->tprof, 0, p->tprof_items * 20 * sizeof(uint64_t)));
         }
         if (p->cw2OT) {
-            SG_ALLOC(p->ws_c2xp, Bz * 2 * p->cw2OT * CW2_THREADS * 16);
+            SG_ALLOC(p->ws_c2xp, Bz * 2 * p->cw2OT * CW2_THREADS * 4);
             SG_ALLOC(p->ws_c2vz, Bz * p->cw2OT * CW2_THREADS * 4);
             SG_ALLOC(p->ws_c2part, Bz * 2 * p->Lblk * 16);
         }
@@ -900,7 +904,7 @@ static Cw2Tables c2tables(const sg_amp_plan *p) {
     tb.cmask = p->c2_cmask; tb.ka = p->c2_ka; tb.oi = p->c2_oi;
     tb.cf = (const float4 *)p->c2_cf; tb.gf = (const float4 *)p->c2_gf;
     tb.cls_ptr = p->r_cls_ptr; tb.cls_ls = p->r_cls_ls; tb.cls2 = p->c2_cls; tb.qpos = p->r_qpos; tb.seg = p->r_seg;
-    tb.xp = (float4 *)p->ws_c2xp; tb.vz = (float *)p->ws_c2vz; tb.wab = (const uint2 *)p->c2_wab; tb.rab = (const uint2 *)p->c2_rab; tb.part = (float4 *)p->ws_c2part;
+    tb.xr = (float *)p->ws_c2xp; tb.vz = (float *)p->ws_c2vz; tb.wab = (const uint2 *)p->c2_wab; tb.rab = (const uint2 *)p->c2_rab; tb.part = (float4 *)p->ws_c2part;
     tb.tprof = p->tprof;  // [2 B][64] stamps (the buffer holds B * Q * 20 >= 128 B words)
     return tb;
 }
@@ -1044,7 +1048,11 @@ static int build_block2(sg_amp_plan *p, const uint32_t *order0, const uint32_t *
     const long long N = p->w, N2 = p->N2;
     const int nT = p->nT, Mc = p->Mc, Mr = p->Mr, M = p->M;
     constexpr int J = 32, T = 1024;
-    std::vector<uint32_t> pos2((size_t)nT * (J / 2) * T, 0u);
+    // per (transform, class): the real LDS index 2 ppos(m1) + component of each column entry of the class in
+    // the padded image, the trash slot (a padding slot, amp_block2.hip B2_TRASH) for the other class's entries
+    constexpr uint32_t TRASH = 2 * 32;
+    static_assert(ppos(32) == 33, "complex position 32 is a padding slot");
+    std::vector<uint32_t> pos2((size_t)nT * 2 * (J / 2) * T, TRASH | (TRASH << 16));
     std::vector<uint32_t> oab((size_t)nT * Mr);
     std::vector<cd> oc((size_t)nT * 2 * Mr * 8), gc;
     std::vector<int32_t> gptr(nT + 1, 0), gi, grow, gk;
@@ -1055,10 +1063,12 @@ static int build_block2(sg_amp_plan *p, const uint32_t *order0, const uint32_t *
         for (int j = 0; j < Mc; ++j) {
             const long long sl = slot_of_pos(o1[j], N);
             const long long m = sl >> 1;
-            const uint32_t lds = (uint32_t)(2 * fsw((int)(m >> 1)) + (int)(sl & 1)) | ((uint32_t)(m & 1) << 15);
+            const uint32_t lds = (uint32_t)(2 * ppos((int)(m >> 1)) + (int)(sl & 1));
+            SG_CHECK_ARG(lds < 65536u, "internal: padded LDS index beyond 16 bits");
             const int l = j / M, rr = j % M;
             const int tid = (l / spw) * 64 + rr / eps, i = (l % spw) * eps + rr % eps;
-            pos2[((size_t)t * (J / 2) + i / 2) * T + tid] |= lds << (16 * (i & 1));
+            uint32_t &w = pos2[(((size_t)t * 2 + (m & 1)) * (J / 2) + i / 2) * T + tid];
+            w = (w & ~(0xffffu << (16 * (i & 1)))) | (lds << (16 * (i & 1)));
         }
         std::vector<std::vector<std::pair<int, cd>>> gcon(N2);
         for (int i = 0; i < Mr; ++i) {
@@ -1078,7 +1088,7 @@ static int build_block2(sg_amp_plan *p, const uint32_t *order0, const uint32_t *
             if (gcon[k].empty()) continue;
             SG_CHECK_ARG(gcon[k].size() <= 4, "internal: >4 contributions to one G slot");
             gk.push_back(k);
-            gloc.push_back((uint16_t)fsw(k & (int)(N2 / 2 - 1)));
+            gloc.push_back((uint16_t)ppos(k & (int)(N2 / 2 - 1)));  // (blk2_az computes it from gk)
             grow.push_back(row_of[t]);
             for (int q = 0; q < 4; ++q) {
                 if (q < (int)gcon[k].size()) { gi.push_back(gcon[k][q].first); gc.push_back(gcon[k][q].second); }
@@ -1087,7 +1097,8 @@ static int build_block2(sg_amp_plan *p, const uint32_t *order0, const uint32_t *
         }
         gptr[t + 1] = (int32_t)gk.size();
     }
-    std::vector<cd> stw;  // stage twiddles of the P-point FFT (fft.hpp lds_fft1_ct, EPT 16)
+    std::vector<cd> stw;  // stage twiddles of the P-point FFT (fft.hpp lds_fft1_ct, EPT 16; unused by the
+                          // sine / cosine stages of amp_block2.hip)
     {
         int radix[8];
         const int ns = fft1_plan(14, 16, radix);
@@ -1302,6 +1313,47 @@ static int build_plan(int ndim, const double *W, int Lr_in, int Lc_in, int L, in
     return SG_OK;
 }
 
+// Active-flag poll, one iteration behind the launches: the copy of the flags
+// after iteration t is requested behind t's launches, iteration t + 1 is
+// launched, and only then does the host wait for the copy -- the GPU works on
+// t + 1 meanwhile, so the poll leaves no idle gap on the stream (a synchronous
+// poll cost ~40 us of idle GPU each time, profiles/README.md).  Decisions
+// taken from the flags after t apply from iteration t + 2 on, at every run and
+// rank count alike (the decode stays deterministic).
+struct ActivePoll {
+    sg_amp_plan *p;
+    int B;
+    hipStream_t s;
+    bool pending = false;
+    int request() {  // behind the launches already on the stream
+        if (!p->poll_ev) SG_HIP(hipEventCreateWithFlags(&p->poll_ev, hipEventDisableTiming));
+        if (p->h_active_cap < B) {
+            if (p->h_active) {
+                SG_HIP(hipEventSynchronize(p->poll_ev));
+                SG_HIP(hipHostFree(p->h_active));
+                p->h_active = nullptr;
+            }
+            SG_HIP(hipHostMalloc((void **)&p->h_active, sizeof(int32_t) * B, hipHostMallocDefault));
+            p->h_active_cap = B;
+        }
+        SG_HIP(hipMemcpyAsync(p->h_active, p->ws_active, sizeof(int32_t) * B, hipMemcpyDeviceToHost, s));
+        SG_HIP(hipEventRecord(p->poll_ev, s));
+        pending = true;
+        return SG_OK;
+    }
+    // the number of active codewords at the last request (-1: none pending)
+    int collect(int *n_active) {
+        *n_active = -1;
+        if (!pending) return SG_OK;
+        SG_HIP(hipEventSynchronize(p->poll_ev));
+        pending = false;
+        int na = 0;
+        for (int b = 0; b < B; ++b) na += p->h_active[b] != 0;
+        *n_active = na;
+        return SG_OK;
+    }
+};
+
 template <typename T>
 static int decode_regular(sg_amp_plan *p, const void *d_y, int B, const int32_t *d_true, double awgn_var, int t_max,
                           double rtol, int phi_method, int32_t *d_map, int32_t *d_tfinal, double *d_nmse,
@@ -1318,8 +1370,8 @@ static int decode_regular(sg_amp_plan *p, const void *d_y, int B, const int32_t 
     pr.atol = 2e-15;  // 2*np.finfo(float).resolution, sparc.py:916
     pr.phi_method = phi_method; pr.t_max = t_max;
     SG_TRY(reg_launch_init(B, p->Lc, t_max, p->ws_nmse, p->ws_active, p->ws_tfinal, s));
-    std::vector<int32_t> act(B);
-    bool cw = std::is_same<T, float>::value && use_cw(p, B);
+    ActivePoll poll{p, B, s};
+    bool cw =std::is_same<T, float>::value && use_cw(p, B);
     p->last_engine = cw ? 2 : 1;
     p->last_handover = -1;
     const char *eng = std::getenv("SG_AMP_ENGINE");
@@ -1340,25 +1392,24 @@ static int decode_regular(sg_amp_plan *p, const void *d_y, int B, const int32_t 
             SG_TRY(reg_launch_az<T>(tb, bf, t, s));
             SG_TRY(reg_launch_merge<T>(tb, bf, sc, pr, t, s));
         }
-        // Poll the active flags: stop once every codeword has stopped, and
-        // hand the remaining iterations to the staged engine once half of the
-        // batch has stopped -- the per-codeword engine keeps one CU per
+        // Poll the active flags (after iterations 3, 7, 11, ..., read one
+        // iteration later, ActivePoll): stop once every codeword has stopped,
+        // and hand the remaining iterations to the staged engine once half of
+        // the batch has stopped -- the per-codeword engine keeps one CU per
         // codeword, so stopped codewords leave CUs idle, while the staged
         // engine spreads the active ones over every CU.  Both keep the same
         // state (s in class order, section statistics, scalars), so the
         // switch is seamless.
-        if (t % 4 == 3 && t + 1 < t_max - 1 && !tb.skip) {
-            SG_HIP(hipMemcpyAsync(act.data(), p->ws_active, sizeof(int32_t) * B, hipMemcpyDeviceToHost, s));
-            SG_HIP(hipStreamSynchronize(s));
-            int na = 0;
-            for (int b = 0; b < B; ++b) na += act[b] != 0;
-            if (na == 0) break;
-            if (cw && !cw_forced && na < handover * B) {
-                cw = false;
-                p->last_handover = t + 1;  // first iteration on the staged engine
-            }
+        int na = -1;
+        SG_TRY(poll.collect(&na));  // the flags after iteration t - 1
+        if (na == 0) break;
+        if (na > 0 && cw && !cw_forced && na < handover * B) {
+            cw = false;
+            p->last_handover = t + 1;  // first iteration on the staged engine
         }
+        if (t % 4 == 3 && t + 2 < t_max - 1 && !tb.skip) SG_TRY(poll.request());
     }
+    if (poll.pending) SG_HIP(hipEventSynchronize(p->poll_ev));
     SG_HIP(hipMemsetAsync(p->ws_argmax, 0x7f, sizeof(int32_t) * B * p->L, s));
     SG_TRY(reg_launch_map<T>(tb, bf, s));
     if (d_map) SG_HIP(hipMemcpyAsync(d_map, p->ws_argmax, sizeof(int32_t) * B * p->L, hipMemcpyDeviceToDevice, s));
@@ -1390,8 +1441,8 @@ static int decode_impl(sg_amp_plan *p, const void *d_y, int B, const int32_t *d_
     const size_t rs = sizeof(T);
     SG_HIP(hipMemsetAsync(p->ws_beta, 0, (size_t)B * p->LM * rs, s));
     SG_TRY(amp_launch_control<T>(tb, bf, sc, pr, 2, 0, s));
-    std::vector<int32_t> act(B);
-    const bool blk = (p->block || p->block2) && sizeof(T) == 4;
+    ActivePoll poll{p, B, s};
+    const bool blk =(p->block || p->block2) && sizeof(T) == 4;
     const BlkTables bt = blk ? btables(p) : BlkTables{};
     p->last_engine = blk ? 3 : 0;
     p->last_handover = -1;
@@ -1412,14 +1463,14 @@ static int decode_impl(sg_amp_plan *p, const void *d_y, int B, const int32_t *d_
             SG_TRY(amp_launch_eta<T>(tb, bf, s));
             SG_TRY(amp_launch_control<T>(tb, bf, sc, pr, 1, t, s));
         }
-        if (t % 4 == 3 && t + 1 < t_max - 1) {  // skip the remaining launches once every codeword stopped
-            SG_HIP(hipMemcpyAsync(act.data(), p->ws_active, sizeof(int32_t) * B, hipMemcpyDeviceToHost, s));
-            SG_HIP(hipStreamSynchronize(s));
-            bool any = false;
-            for (int b = 0; b < B; ++b) any |= act[b] != 0;
-            if (!any) break;
-        }
+        // skip the remaining launches once every codeword stopped (ActivePoll: the flags after
+        // iterations 3, 7, 11, ..., read one iteration later)
+        int na = -1;
+        SG_TRY(poll.collect(&na));
+        if (na == 0) break;
+        if (t % 4 == 3 && t + 2 < t_max - 1) SG_TRY(poll.request());
     }
+    if (poll.pending) SG_HIP(hipEventSynchronize(p->poll_ev));
     if (d_map) SG_HIP(hipMemcpyAsync(d_map, p->ws_argmax, sizeof(int32_t) * B * p->L, hipMemcpyDeviceToDevice, s));
     if (d_tfinal) SG_HIP(hipMemcpyAsync(d_tfinal, p->ws_tfinal, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
     if (d_nmse) SG_HIP(hipMemcpyAsync(d_nmse, p->ws_nmse, sizeof(double) * B * t_max * p->Lc, hipMemcpyDeviceToDevice, s));
@@ -1549,6 +1600,11 @@ int sg_amp_plan_destroy(sg_amp_plan *p) {
     plan_free_ws(p);
     for (void *a : p->allocs) hipFree(a);
     if (p->tprof) hipFree(p->tprof);
+    if (p->poll_ev) {
+        hipEventSynchronize(p->poll_ev);  // (a copy into h_active may still be in flight)
+        hipEventDestroy(p->poll_ev);
+    }
+    if (p->h_active) hipHostFree(p->h_active);
     delete p;
     return SG_OK;
 }

@@ -272,6 +272,17 @@ __host__ __device__ __forceinline__ int fsw(int i) { return i ^ ((i >> 4) & 15);
 // element i at fpad(i) = i + i/16, so one-thread-per-segment reads spread
 // over the banks.
 __host__ __device__ __forceinline__ int fpad(int i) { return i + (i >> 4); }
+// Padded layout (PAD = true in the compile-time stages below; the split
+// engine's image layout, amp.hpp c2pos): element i at ppos(i) = i + i/32.
+// Every load and store of a stage is then a per-thread base plus a constant
+// (ppos(b + c) = ppos(b) + ppos_off(...)), so no swizzle arithmetic per
+// element; the price is one padding slot per 32 elements.
+__host__ __device__ constexpr int ppos(int i) { return i + (i >> 5); }
+// ppos(b + NS r) - ppos(b) for the bases b of stockham1_stage_ct: NS = 1 with
+// b a multiple of R (R | 32), NS = 16 with b mod 32 < 16, NS a multiple of 32
+__host__ __device__ constexpr int ppos_off(int NS, int r) {
+    return NS == 1 ? r : NS == 16 ? 16 * r + (r >> 1) : r * (NS + NS / 32);
+}
 
 // Stage twiddles w^(r k), r < R, of butterfly k are rebuilt from TWN(R) table
 // entries per k (a twentieth of the table traffic of R - 1 entries, and few
@@ -485,22 +496,25 @@ __device__ __forceinline__ void fft1_tw_load_ct(const cx<T> *__restrict__ stw, i
     }
 }
 
-template <typename T, bool INV, int R, int EPT, int LOG2N, int LOG2NS>
+template <typename T, bool INV, int R, int EPT, int LOG2N, int LOG2NS, bool PAD = false>
 __device__ __forceinline__ void stockham1_stage_ct(cx<T> *d, const cx<T> *wl, int tid) {
     constexpr int NB = EPT / R;
     constexpr int LR = (R == 2) ? 1 : (R == 4) ? 2 : (R == 8) ? 3 : 4;
     constexpr int NBF = 1 << (LOG2N - LR);
     constexpr int NS = 1 << LOG2NS;
     constexpr int NTHR = (1 << LOG2N) / EPT;
+    static_assert(!PAD || ((NS == 1 || NS == 16 || NS % 32 == 0) && NBF % 32 == 0 && 32 % R == 0),
+                  "padded layout: stage offsets are constants only for these strides");
     cx<T> v[EPT];
     int base_out[NB];
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
         const int j = tid + i * NTHR;
         const int k = j & (NS - 1);
-        const int jp = fsw(j);
+        const int jp = PAD ? ppos(j) : fsw(j);
 #pragma unroll
-        for (int r = 0; r < R; ++r) v[i * R + r] = d[(NBF % 256 == 0) ? jp + r * NBF : fsw(j + r * NBF)];
+        for (int r = 0; r < R; ++r)
+            v[i * R + r] = d[PAD ? jp + r * (NBF + NBF / 32) : (NBF % 256 == 0) ? jp + r * NBF : fsw(j + r * NBF)];
         if constexpr (LOG2NS > 0) tw_apply<T, INV, R>(wl + i * tw_per_k(R), &v[i * R]);
         dftR<T, INV, R>(&v[i * R]);
         base_out[i] = ((j - k) << LR) + k;
@@ -508,9 +522,10 @@ __device__ __forceinline__ void stockham1_stage_ct(cx<T> *d, const cx<T> *wl, in
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-        const int bp = fsw(base_out[i]);
+        const int bp = PAD ? ppos(base_out[i]) : fsw(base_out[i]);
 #pragma unroll
-        for (int r = 0; r < R; ++r) d[(NS % 256 == 0) ? bp + r * NS : fsw(base_out[i] + r * NS)] = v[i * R + r];
+        for (int r = 0; r < R; ++r)
+            d[PAD ? bp + ppos_off(NS, r) : (NS % 256 == 0) ? bp + r * NS : fsw(base_out[i] + r * NS)] = v[i * R + r];
     }
     __syncthreads();
 }
@@ -541,7 +556,7 @@ __device__ __forceinline__ void lds_fft1_ct(cx<T> *d, const cx<T> *__restrict__ 
 // hardware sine / cosine instead of the table (single precision): the
 // argument is in revolutions and (e k mod Ns R) / (Ns R) is exact, and no
 // global load sits between the transform's barriers.
-template <bool INV, int EPT, int LOG2N, int ST>
+template <bool INV, int EPT, int LOG2N, int ST, bool PAD = false>
 __device__ __forceinline__ void fft1_stage_sincos(cx<float> *d, int tid) {
     constexpr int R = fft1_radix_ct(LOG2N, EPT, ST), LNS = fft1_log2ns_ct(LOG2N, EPT, ST);
     constexpr int NB = EPT / R, TWN = tw_per_k(R), NTHR = (1 << LOG2N) / EPT;
@@ -559,14 +574,14 @@ __device__ __forceinline__ void fft1_stage_sincos(cx<float> *d, int tid) {
             }
         }
     }
-    stockham1_stage_ct<float, INV, R, EPT, LOG2N, LNS>(d, wl, tid);
+    stockham1_stage_ct<float, INV, R, EPT, LOG2N, LNS, PAD>(d, wl, tid);
 }
-// stages ST0 .. ST1 - 1
-template <bool INV, int EPT, int LOG2N, int ST0, int ST1>
+// stages ST0 .. ST1 - 1 (PAD: element i at ppos(i))
+template <bool INV, int EPT, int LOG2N, int ST0, int ST1, bool PAD = false>
 __device__ __forceinline__ void lds_fft1_sincos(cx<float> *d, int tid) {
     if constexpr (ST0 < ST1) {
-        fft1_stage_sincos<INV, EPT, LOG2N, ST0>(d, tid);
-        lds_fft1_sincos<INV, EPT, LOG2N, ST0 + 1, ST1>(d, tid);
+        fft1_stage_sincos<INV, EPT, LOG2N, ST0, PAD>(d, tid);
+        lds_fft1_sincos<INV, EPT, LOG2N, ST0 + 1, ST1, PAD>(d, tid);
     }
 }
 

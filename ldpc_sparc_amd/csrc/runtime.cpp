@@ -86,6 +86,7 @@ struct ProfRec {
     hipEvent_t a, b;
 };
 static bool g_prof_on = false;
+static int g_prof_level = 1;  // 2: the per-iteration scope only (no per-kernel events inside it)
 static std::vector<ProfRec> g_prof_pending;
 static std::vector<hipEvent_t> g_ev_pool;
 static double g_prof_ms[SG_PH_COUNT] = {0};
@@ -102,8 +103,13 @@ static hipEvent_t ev_get() {
     return e;
 }
 
+// the split engine's per-kernel scopes, nested in its per-iteration scope (SG_PH_AMP_CW)
+static bool prof_inner(int phase) {
+    return phase == SG_PH_CW2_AB || phase == SG_PH_CW2_AZ || phase == SG_PH_CW2_CTRL;
+}
+
 int prof_begin(int phase, hipStream_t s) {
-    if (!g_prof_on) return -1;
+    if (!g_prof_on || (g_prof_level >= 2 && prof_inner(phase))) return -1;
     std::lock_guard<std::mutex> lk(g_mu);
     ProfRec r{phase, ev_get(), ev_get()};
     if (!r.a || !r.b) return -1;
@@ -215,6 +221,7 @@ int sg_stream_destroy(void *stream) {
 int sg_profile_enable(int on) {
     std::lock_guard<std::mutex> lk(g_mu);
     g_prof_on = on != 0;
+    g_prof_level = on;
     return SG_OK;
 }
 

@@ -501,9 +501,10 @@ def test_auto_engine_handover_matches_staged(monkeypatch, handover):
     assert last["engine"] == 2 and not last["companion"]
     if handover is not None:
         # the codewords of this design stop after 8-12 iterations; the active
-        # flags are polled every 4 iterations, so with 99 % the hand-over
-        # happens at the second poll and iterations 9.. run on the staged engine
-        assert last["handover_iter"] == 8 and int(ta.max()) > 8, (last, np.bincount(ta))
+        # flags are copied after iterations 3, 7, ... and read one iteration
+        # later, so with 99 % the hand-over follows the second copy and
+        # iterations 10.. run on the staged engine
+        assert last["handover_iter"] == 9 and int(ta.max()) > 9, (last, np.bincount(ta))
     monkeypatch.delenv("SG_AMP_HANDOVER", raising=False)
     monkeypatch.setenv("SG_AMP_ENGINE", "staged")
     ms, ts, ns, _ = sparc.amp_decode_batch(Y, op, 1.0, 25, true_idx=true, precision=_native.SG_F32)
