@@ -9,7 +9,7 @@
 //
 // One workgroup owns one column block c of one codeword and runs the omega
 // transforms of that column back to back, each entirely in LDS (Makhoul-packed
-// N2-point FFT, natural order at fsw positions):
+// N2-point FFT, natural order in the padded layout of fft.hpp ppos):
 //   Ab       beta_c (registers) -> for each transform (r, c): scatter by
 //            order1, forward FFT, the Mr needed outputs Re(c1 H[a] + c2 conj
 //            H[b]) -> rbuf[t] (summed per row block in a fixed order by the
@@ -49,16 +49,17 @@ __device__ __forceinline__ int bk_wave_min(int v) {
     return v;
 }
 
-// LDS: the FFT image, then the staged positions of one transform (blk_az);
-// the per-wave partials of the section reductions overlay the image
-size_t blk_lds_bytes(int Mc) {
-    return (size_t)(1 << BK_LOG2N) * sizeof(cx<float>) + (size_t)(BK_J / 2) * BK_THREADS * sizeof(uint32_t);
-}
+// LDS: the FFT image in the padded layout (element i at ppos(i) = i + i/32:
+// every FFT stage access a per-thread base plus a constant, no swizzle
+// arithmetic)
+constexpr int BK_IMG = ppos(1 << BK_LOG2N);  // complex slots
+size_t blk_lds_bytes(int Mc) { return (size_t)BK_IMG * sizeof(cx<float>); }
 
 __device__ __forceinline__ void bk_clear(unsigned char *smem, int tid) {
+    constexpr int N16 = BK_IMG * (int)sizeof(cx<float>) / 16;  // (8448: 8 per thread and a quarter)
 #pragma unroll
-    for (int i = 0; i < (1 << BK_LOG2N) * (int)sizeof(cx<float>) / 16 / BK_THREADS; ++i)
-        reinterpret_cast<uint4 *>(smem)[tid + i * BK_THREADS] = uint4{0, 0, 0, 0};
+    for (int i = 0; i < (N16 + BK_THREADS - 1) / BK_THREADS; ++i)
+        if (tid + i * BK_THREADS < N16) reinterpret_cast<uint4 *>(smem)[tid + i * BK_THREADS] = uint4{0, 0, 0, 0};
 }
 
 // The thread index as a value the compiler cannot see through: the FFT's LDS
@@ -95,14 +96,14 @@ __device__ __forceinline__ uint32_t bk_pos(const uint32_t *pv, int i) { return (
 // needed outputs.
 __device__ __forceinline__ void bk_fwd_stages(cx<float> *d, const cx<float> *__restrict__ stw, int tid) {
     if constexpr (SG_BLK_SINCOS & 1) {
-        lds_fft1_sincos<false, 16, BK_LOG2N, 0, 3>(d, tid);
+        lds_fft1_sincos<false, 16, BK_LOG2N, 0, 3, true>(d, tid);
     } else {
         cx<float> w0[1], w1[6], w2[6];
         fft1_tw_load_ct<float, 16, BK_LOG2N, 1>(stw, tid, w1);
-        stockham1_stage_ct<float, false, 16, 16, BK_LOG2N, 0>(d, w0, tid);
+        stockham1_stage_ct<float, false, 16, 16, BK_LOG2N, 0, true>(d, w0, tid);
         fft1_tw_load_ct<float, 16, BK_LOG2N, 2>(stw, tid, w2);
-        stockham1_stage_ct<float, false, 16, 16, BK_LOG2N, 4>(d, w1, tid);
-        stockham1_stage_ct<float, false, 16, 16, BK_LOG2N, 8>(d, w2, tid);
+        stockham1_stage_ct<float, false, 16, 16, BK_LOG2N, 4, true>(d, w1, tid);
+        stockham1_stage_ct<float, false, 16, 16, BK_LOG2N, 8, true>(d, w2, tid);
     }
 }
 
@@ -137,8 +138,8 @@ __device__ __forceinline__ void bk_ab_column(const BlkTables &tb, const AmpBufs<
             const int ja = ab & 0xffffu, jb = ab >> 16;
             float acc = 0.f;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const cx<float> ya = d[fsw(ja + 4096 * q)], yb = d[fsw(jb + 4096 * q)];
+            for (int q = 0; q < 4; ++q) {  // ppos(j + 4096 q) = ppos(j) + 4224 q for j < 4096
+                const cx<float> ya = d[ppos(ja) + 4224 * q], yb = d[ppos(jb) + 4224 * q];
                 const cx<float> al = oc[8 * i + q], be = oc[8 * i + 4 + q];
                 acc += (al.x * ya.x - al.y * ya.y) + (be.x * yb.x + be.y * yb.y);
             }
@@ -213,9 +214,6 @@ __global__ __launch_bounds__(BK_THREADS) void blk_az(BlkTables tb, AmpBufs<float
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     cx<float> *d = reinterpret_cast<cx<float> *>(smem);
     float *dr = reinterpret_cast<float *>(smem);
-    // positions of the current transform's column entries, staged in LDS
-    // beside the image (held in registers across the FFT they would spill)
-    uint32_t *pl = reinterpret_cast<uint32_t *>(smem + (size_t)(1 << BK_LOG2N) * sizeof(cx<float>));
     const int c = blockIdx.x, cw = blockIdx.y, tid = threadIdx.x;
     if (!bf.active[cw]) return;
     float u[BK_J];
@@ -226,9 +224,7 @@ __global__ __launch_bounds__(BK_THREADS) void blk_az(BlkTables tb, AmpBufs<float
     for (int q = tb.col_ptr[c]; q < tb.col_ptr[c + 1]; ++q) {
         const int t = tb.col_t[q];
         const int tl = bk_opaque(tid);
-        // positions and G slots (from z / phi, <= 4 terms), in flight while the image clears
-        uint32_t pv[BK_J / 2];
-        bk_pos_load(tb, t, tl, pv);
+        // G slots (from z / phi, <= 4 terms), in flight while the image clears
         const int g0 = tb.gptr[t], ng = tb.gptr[t + 1] - g0;
         cx<float> gv[2];
         uint32_t gl[2];
@@ -241,21 +237,21 @@ __global__ __launch_bounds__(BK_THREADS) void blk_az(BlkTables tb, AmpBufs<float
             }
         }
         bk_clear(smem, tl);
-#pragma unroll
-        for (int i = 0; i < BK_J / 2; ++i) pl[i * BK_THREADS + tl] = pv[i];
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < 2; ++k)
             if (tl + k * BK_THREADS < ng) d[gl[k]] = gv[k];
         for (int g = tl + 2 * BK_THREADS; g < ng; g += BK_THREADS) d[tb.gloc[g0 + g]] = bk_gslot(tb, bf, cw, g0 + g);
         __syncthreads();
-        if (!(tb.skip & 2)) {
-            if constexpr (SG_BLK_SINCOS & 2) lds_fft1_sincos<true, 16, BK_LOG2N, 0, 4>(d, tl);
-            else lds_fft1_ct<float, true, 16, BK_LOG2N>(d, tb.stw, tl);
-        }
+        // the positions of this transform's column entries are requested before the last stage (in flight
+        // during it; the padded image leaves no LDS to stage them in, and held across the whole FFT they
+        // would spill)
+        uint32_t pv[BK_J / 2];
+        if (!(tb.skip & 2)) lds_fft1_sincos<true, 16, BK_LOG2N, 0, 3, true>(d, tl);
+        bk_pos_load(tb, t, tl, pv);
+        if (!(tb.skip & 2)) lds_fft1_sincos<true, 16, BK_LOG2N, 3, 4, true>(d, tl);
 #pragma unroll
-        for (int i = 0; i < BK_J; ++i)
-            u[i] += dr[(pl[(i >> 1) * BK_THREADS + tl] >> (16 * (i & 1))) & 0xffffu];
+        for (int i = 0; i < BK_J; ++i) u[i] += dr[bk_pos(pv, i)];
         __syncthreads();
     }
     if (tb.skip & 1) return;  // timing ablation only

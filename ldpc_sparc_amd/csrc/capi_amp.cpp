@@ -965,7 +965,7 @@ static RegBufs<T> rbufs(const sg_amp_plan *p, int B, const void *y) {
 
 // Tables of the block engine (amp_block.hip): per transform, the LDS position
 // of every column entry, the output gathers and the G slots, all in the
-// natural-order FFT image of lds_fft1_ct (fsw positions).
+// natural-order FFT image in the padded layout (fft.hpp ppos).
 static int build_block(sg_amp_plan *p, const uint32_t *order0, const uint32_t *order1,
                        const std::vector<double> &t_scale, const std::vector<int32_t> &row_of) {
     const long long N = p->w, N2 = p->N2;
@@ -979,7 +979,8 @@ static int build_block(sg_amp_plan *p, const uint32_t *order0, const uint32_t *o
         const uint32_t *o0 = order0 + (size_t)t * Mr, *o1 = order1 + (size_t)t * Mc;
         for (int j = 0; j < Mc; ++j) {
             const long long sl = slot_of_pos(o1[j], N);
-            const uint32_t lds = (uint32_t)(2 * fsw((int)(sl >> 1)) + (int)(sl & 1));
+            const uint32_t lds = (uint32_t)(2 * ppos((int)(sl >> 1)) + (int)(sl & 1));
+            SG_CHECK_ARG(lds < 65536u, "internal: padded LDS index beyond 16 bits");
             // owner (thread, entry) of column entry j: amp_block.hip bk_j
             const int M = p->M, eps = M / 64, spw = 1024 / M;
             const int l = j / M, rr = j % M;
@@ -1002,7 +1003,7 @@ static int build_block(sg_amp_plan *p, const uint32_t *order0, const uint32_t *o
         for (int k = 0; k < N2; ++k) {
             if (gcon[k].empty()) continue;
             SG_CHECK_ARG(gcon[k].size() <= 4, "internal: >4 contributions to one G slot");
-            gloc.push_back((uint16_t)fsw(k));
+            gloc.push_back((uint16_t)ppos(k));
             grow.push_back(row_of[t]);
             for (int q = 0; q < 4; ++q) {
                 if (q < (int)gcon[k].size()) { gi.push_back(gcon[k][q].first); gc.push_back(gcon[k][q].second); }
