@@ -58,9 +58,10 @@ struct BlkTables {
     const cx<float> *gc;      // [4] per slot: coefficient
     const cx<float> *stw;     // per-stage twiddles of the N2-point FFT (fft.hpp lds_fft1_ct, EPT 16)
     int skip;                 // timing ablation only (SG_AMP_SKIP): 1 sections, 2 inverse FFT
+    int log2p;                // two-class engine: class size P = 2^log2p (13: C4's w = 2^15, 14: w = 2^16)
 };
 size_t blk_lds_bytes(int Mc);
-size_t blk2_lds_bytes();
+size_t blk2_lds_bytes(int log2p);
 
 // Per-batch device buffers.
 template <typename T>

@@ -26,16 +26,27 @@
 
 namespace sg {
 
-constexpr int B2_THREADS = 1024;
-constexpr int B2_LOG2P = 14, B2_P = 1 << B2_LOG2P;
-constexpr int B2_J = 32;  // column entries per thread (Mc = 32768)
-constexpr int B2_JR = 32;  // of which blk2_ab holds in registers (any rest in the LDS past the image)
-// The class image in the padded layout of fft.hpp ppos (element i at i + i/32:
-// every FFT stage access is a per-thread base plus a constant, no swizzle
-// arithmetic); a padding slot -- never written by the rows or the FFT stages,
-// so zero after b2_clear -- is the trash slot of the position tables.
-constexpr int B2_IMG = ppos(B2_P);       // complex slots of the padded image
-constexpr int B2_TRASH = 2 * 32;         // real index of the padding slot at complex position 32
+// Two geometries (template parameter LP = log2 P, 16 image values per thread):
+//   LP = 14: the notebook's w = 2^16, Mc = 2^15, 1024 threads, one workgroup per CU;
+//   LP = 13: C4's w = 2^15, Mc = 2^14 as two classes of 2^13 points, 512 threads
+//            and a 66 KB image, so two workgroups share a CU and one's barriers
+//            and LDS latency run beside the other's transform (the single-class
+//            engine, amp_block.hip, holds 132 KB and runs alone on its CU).
+template <int LP>
+struct B2G {
+    static constexpr int P = 1 << LP;
+    static constexpr int THREADS = P / 16;
+    // The class image in the padded layout of fft.hpp ppos (element i at i + i/32:
+    // every FFT stage access is a per-thread base plus a constant, no swizzle
+    // arithmetic)
+    static constexpr int IMG = ppos(P);  // complex slots of the padded image
+    static constexpr int RF = P / 4096;  // radix of the last stage, folded into the output coefficients
+    static_assert(RF == 2 || RF == 4, "P = 2^13 or 2^14");
+};
+constexpr int B2_J = 32;  // column entries per thread (Mc = 2 P = 32 threads), all held in registers
+// a padding slot -- never written by the rows or the FFT stages, so zero after
+// b2_clear -- is the trash slot of the position tables
+constexpr int B2_TRASH = 2 * 32;  // real index of the padding slot at complex position 32
 static_assert(ppos(B2_TRASH / 2) == B2_TRASH / 2 + 1, "the trash slot is a padding slot (capi_amp.cpp build_block2)");
 
 namespace {
@@ -63,11 +74,12 @@ __device__ __forceinline__ int b2_opaque(int v) {
     return v;
 }
 
+template <int LP>
 __device__ __forceinline__ void b2_clear(unsigned char *smem, int tid) {
-    constexpr int N16 = B2_IMG * (int)sizeof(cx<float>) / 16;  // (8448: 8 per thread and a quarter)
+    constexpr int T = B2G<LP>::THREADS, N16 = B2G<LP>::IMG * (int)sizeof(cx<float>) / 16;  // (8 per thread and a quarter)
 #pragma unroll
-    for (int i = 0; i < (N16 + B2_THREADS - 1) / B2_THREADS; ++i)
-        if (tid + i * B2_THREADS < N16) reinterpret_cast<uint4 *>(smem)[tid + i * B2_THREADS] = uint4{0, 0, 0, 0};
+    for (int i = 0; i < (N16 + T - 1) / T; ++i)
+        if (tid + i * T < N16) reinterpret_cast<uint4 *>(smem)[tid + i * T] = uint4{0, 0, 0, 0};
 }
 
 // Column entry i (< 32) of thread tid: wavefront w owns sections
@@ -84,55 +96,61 @@ __device__ __forceinline__ int b2_j(int tid, int i) {
 // real LDS index in the image of class m2 (2 ppos(m1) + component; B2_TRASH
 // for the entries of the other class) of the thread's column entries of
 // transform t, packed in pairs
+template <int LP>
 __device__ __forceinline__ void b2_pos_load(const BlkTables &tb, int t, int m2, int tid, uint32_t *pv) {
-    const uint32_t *p2 = tb.pos2 + ((size_t)t * 2 + m2) * (B2_J / 2) * B2_THREADS;
+    constexpr int T = B2G<LP>::THREADS;
+    const uint32_t *p2 = tb.pos2 + ((size_t)t * 2 + m2) * (B2_J / 2) * T;
 #pragma unroll
-    for (int i = 0; i < B2_J / 2; ++i) pv[i] = p2[i * B2_THREADS + tid];
+    for (int i = 0; i < B2_J / 2; ++i) pv[i] = p2[i * T + tid];
 }
 __device__ __forceinline__ uint32_t b2_pos(const uint32_t *pv, int i) { return (pv[i >> 1] >> (16 * (i & 1))) & 0xffffu; }
 
 // the first three stages (radix 16) of the P-point FFT over the padded image,
 // twiddles from the hardware sine / cosine (no table entries in flight: blk2_ab
 // holds beta_c in registers; with the table prefetch it spills)
+template <int LP>
 __device__ __forceinline__ void b2_fwd_stages(cx<float> *d, int tid) {
-    lds_fft1_sincos<false, 16, B2_LOG2P, 0, 3, true>(d, tid);
+    lds_fft1_sincos<false, 16, LP, 0, 3, true>(d, tid);
 }
 
 }  // namespace
 
-size_t blk2_lds_bytes() { return (size_t)B2_IMG * sizeof(cx<float>) + (size_t)(B2_J - B2_JR) * B2_THREADS * 4; }
+size_t blk2_lds_bytes(int log2p) {
+    return log2p == 13 ? (size_t)B2G<13>::IMG * sizeof(cx<float>) : (size_t)B2G<14>::IMG * sizeof(cx<float>);
+}
 
 // ------------------------------------------------------------------ Ab
 // The column's forward transforms from beta_c in registers (bv[i] = beta_c at
 // b2_j(tid, i)): for each transform and class, scatter -> three radix-16
-// stages -> the needed outputs (last radix-4 stage and class factor folded into
+// stages -> the needed outputs (last radix-RF stage and class factor folded into
 // the coefficients), summed over the classes in registers -> rbuf[t]
+template <int LP>
 __device__ __forceinline__ void b2_ab_column(const BlkTables &tb, const AmpBufs<float> &bf, int c, int cw, int tid,
                                              const float *bv, unsigned char *smem) {
     cx<float> *d = reinterpret_cast<cx<float> *>(smem);
     float *dr = reinterpret_cast<float *>(smem);
     for (int q = tb.col_ptr[c]; q < tb.col_ptr[c + 1]; ++q) {
         const int t = tb.col_t[q];
-        float acc = 0.f;  // output tid (Mr <= 1024), summed over the two classes
+        float acc = 0.f;  // output tid (Mr <= THREADS), summed over the two classes
         for (int m2 = 0; m2 < 2; ++m2) {
             const int tl = b2_opaque(tid);
             // the positions, in flight while the image clears
             uint32_t pv[B2_J / 2];
-            b2_pos_load(tb, t, m2, tl, pv);
-            b2_clear(smem, tl);
+            b2_pos_load<LP>(tb, t, m2, tl, pv);
+            b2_clear<LP>(smem, tl);
             __syncthreads();
 #pragma unroll
             for (int i = 0; i < B2_J; ++i) dr[b2_pos(pv, i)] = bv[i];  // (the other class's entries: trash slot)
             __syncthreads();
-            b2_fwd_stages(d, tl);
-            // X_i += Re(sum_r al_r Y[a mod 4096 + 4096 r] + be_r conj Y[b mod ...]):
-            // the radix-4 stage and w_N2^(m2 k) are in the coefficients
+            b2_fwd_stages<LP>(d, tl);
+            // X_i += Re(sum_r al_r Y[a mod 4096 + 4096 r] + be_r conj Y[b mod ...]), r < RF:
+            // the last stage and w_N2^(m2 k) are in the coefficients
             if (tl < tb.Mr) {
                 const uint32_t ab = tb.oab[(size_t)t * tb.Mr + tl];
                 const int ja = ab & 0xffffu, jb = ab >> 16;
                 const cx<float> *oc = tb.oc + (((size_t)t * 2 + m2) * tb.Mr + tl) * 8;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {  // ppos(j + 4096 r) = ppos(j) + 4224 r for j < 4096
+                for (int r = 0; r < B2G<LP>::RF; ++r) {  // ppos(j + 4096 r) = ppos(j) + 4224 r for j < 4096
                     const cx<float> ya = d[ppos(ja) + 4224 * r], yb = d[ppos(jb) + 4224 * r];
                     const cx<float> al = oc[r], be = oc[4 + r];
                     acc += (al.x * ya.x - al.y * ya.y) + (be.x * yb.x + be.y * yb.y);
@@ -146,8 +164,8 @@ __device__ __forceinline__ void b2_ab_column(const BlkTables &tb, const AmpBufs<
 
 // Standalone Ab (beta_c read once for all the column's transforms and
 // classes); iterations after the first run it inside the previous blk2_az
-template <int EPS>
-__global__ __launch_bounds__(B2_THREADS) void blk2_ab(BlkTables tb, AmpBufs<float> bf) {
+template <int LP, int EPS>
+__global__ __launch_bounds__(B2G<LP>::THREADS, 4) void blk2_ab(BlkTables tb, AmpBufs<float> bf) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int c = blockIdx.x, cw = blockIdx.y, tid = threadIdx.x;
     if (!bf.active[cw]) return;
@@ -155,12 +173,14 @@ __global__ __launch_bounds__(B2_THREADS) void blk2_ab(BlkTables tb, AmpBufs<floa
     float bv[B2_J];
 #pragma unroll
     for (int i = 0; i < B2_J; ++i) bv[i] = beta[b2_j<EPS>(tid, i)];
-    b2_ab_column(tb, bf, c, cw, tid, bv, smem);
+    b2_ab_column<LP>(tb, bf, c, cw, tid, bv, smem);
 }
 
 // ------------------------------------------------------------------ Az + eta
-template <int EPS>
-__global__ __launch_bounds__(B2_THREADS) void blk2_az(BlkTables tb, AmpBufs<float> bf, const cx<float> *gbuf,
+// (__launch_bounds__ with 4 waves per SIMD: 128 VGPRs, so two 512-thread
+// workgroups share a CU at LP = 13)
+template <int LP, int EPS>
+__global__ __launch_bounds__(B2G<LP>::THREADS, 4) void blk2_az(BlkTables tb, AmpBufs<float> bf, const cx<float> *gbuf,
                                                       int do_ab) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     cx<float> *d = reinterpret_cast<cx<float> *>(smem);
@@ -171,18 +191,19 @@ __global__ __launch_bounds__(B2_THREADS) void blk2_az(BlkTables tb, AmpBufs<floa
 #pragma unroll
     for (int i = 0; i < B2_J; ++i) u[i] = 0.f;
     const cx<float> *gcw = gbuf + (size_t)cw * tb.ngs;
-    const float inv_n2 = 1.0f / (float)(2 * B2_P);
+    constexpr int T = B2G<LP>::THREADS, P = B2G<LP>::P;
+    const float inv_n2 = 1.0f / (float)(2 * P);
     for (int q = tb.col_ptr[c]; q < tb.col_ptr[c + 1]; ++q) {
         const int t = tb.col_t[q];
         const int g0 = tb.gptr[t], ng = tb.gptr[t + 1] - g0;
         for (int m2 = 0; m2 < 2; ++m2) {
             const int tl = b2_opaque(tid);
-            b2_clear(smem, tl);
+            b2_clear<LP>(smem, tl);
             __syncthreads();
             // rows of class m2: U[k1] = sum over k = k1 mod P of G[k] conj(w_N2^(m2 k));
             // at most two slots (k1, k1 + P) share a row, and two float additions
             // onto a zero commute, so the atomic sum is deterministic
-            for (int g = tl; g < ng; g += B2_THREADS) {
+            for (int g = tl; g < ng; g += T) {
                 const int k = tb.gk[g0 + g];
                 cx<float> v = gcw[g0 + g];
                 if (m2) {
@@ -190,15 +211,15 @@ __global__ __launch_bounds__(B2_THREADS) void blk2_az(BlkTables tb, AmpBufs<floa
                     const float cs = __builtin_amdgcn_cosf(x), sn = __builtin_amdgcn_sinf(x);
                     v = {v.x * cs - v.y * sn, v.x * sn + v.y * cs};
                 }
-                cx<float> *dst = &d[ppos(k & (B2_P - 1))];
+                cx<float> *dst = &d[ppos(k & (P - 1))];
                 atomicAdd(&dst->x, v.x);
                 atomicAdd(&dst->y, v.y);
             }
             __syncthreads();
             // (stage twiddles from the hardware sine / cosine: no table entries in flight, u[] stays in registers)
-            lds_fft1_sincos<true, 16, B2_LOG2P, 0, 4, true>(d, tl);
+            lds_fft1_sincos<true, 16, LP, 0, 4, true>(d, tl);
             uint32_t pv[B2_J / 2];
-            b2_pos_load(tb, t, m2, tl, pv);
+            b2_pos_load<LP>(tb, t, m2, tl, pv);
 #pragma unroll
             for (int i = 0; i < B2_J; ++i) u[i] += dr[b2_pos(pv, i)];  // (the other class's entries read the
                                                                       // zero trash slot)
@@ -271,53 +292,63 @@ __global__ __launch_bounds__(B2_THREADS) void blk2_az(BlkTables tb, AmpBufs<floa
     // computes one Ab nobody reads)
     if (do_ab) {
         __syncthreads();  // the image is free
-        b2_ab_column(tb, bf, c, cw, tid, bv, smem);
+        b2_ab_column<LP>(tb, bf, c, cw, tid, bv, smem);
     }
 }
 
-template <int EPS>
+template <int LP, int EPS>
 static int blk2_set_attrs(size_t lds) {
     static size_t done = 0;
     if (done >= lds) return SG_OK;
-    SG_HIP(hipFuncSetAttribute((const void *)blk2_ab<EPS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    SG_HIP(hipFuncSetAttribute((const void *)blk2_az<EPS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    SG_HIP(hipFuncSetAttribute((const void *)blk2_ab<LP, EPS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    SG_HIP(hipFuncSetAttribute((const void *)blk2_az<LP, EPS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     done = lds;
     return SG_OK;
 }
 
 // section size M = 64 EPS, 64 <= M <= 2048
-#define B2_EPS_DISPATCH(M, F, ...)                                                              \
+#define B2_EPS_DISPATCH(LP, M, F, ...)                                                          \
     switch (M) {                                                                                \
-    case 64: F<1>(__VA_ARGS__); break;                                                          \
-    case 128: F<2>(__VA_ARGS__); break;                                                         \
-    case 256: F<4>(__VA_ARGS__); break;                                                         \
-    case 512: F<8>(__VA_ARGS__); break;                                                         \
-    case 1024: F<16>(__VA_ARGS__); break;                                                       \
-    case 2048: F<32>(__VA_ARGS__); break;                                                       \
+    case 64: F<LP, 1>(__VA_ARGS__); break;                                                      \
+    case 128: F<LP, 2>(__VA_ARGS__); break;                                                     \
+    case 256: F<LP, 4>(__VA_ARGS__); break;                                                     \
+    case 512: F<LP, 8>(__VA_ARGS__); break;                                                     \
+    case 1024: F<LP, 16>(__VA_ARGS__); break;                                                   \
+    case 2048: F<LP, 32>(__VA_ARGS__); break;                                                   \
     default: return fail(SG_ERR_UNSUPPORTED, "block engine (two classes): section size M=%d", M); \
     }
 
-template <int EPS>
+template <int LP, int EPS>
 static void b2_launch_ab(const BlkTables &tb, const AmpBufs<float> &bf, size_t lds, hipStream_t s, int *rc) {
-    *rc = blk2_set_attrs<EPS>(lds);
-    if (*rc == SG_OK) hipLaunchKernelGGL(blk2_ab<EPS>, dim3(tb.Lc, bf.B), dim3(B2_THREADS), lds, s, tb, bf);
+    *rc = blk2_set_attrs<LP, EPS>(lds);
+    if (*rc == SG_OK)
+        hipLaunchKernelGGL((blk2_ab<LP, EPS>), dim3(tb.Lc, bf.B), dim3(B2G<LP>::THREADS), lds, s, tb, bf);
 }
-template <int EPS>
+template <int LP, int EPS>
 static void b2_launch_az(const BlkTables &tb, const AmpBufs<float> &bf, const cx<float> *gbuf, int do_ab, size_t lds,
                          hipStream_t s, int *rc) {
-    *rc = blk2_set_attrs<EPS>(lds);
+    *rc = blk2_set_attrs<LP, EPS>(lds);
     if (*rc == SG_OK)
-        hipLaunchKernelGGL(blk2_az<EPS>, dim3(tb.Lc, bf.B), dim3(B2_THREADS), lds, s, tb, bf, gbuf, do_ab);
+        hipLaunchKernelGGL((blk2_az<LP, EPS>), dim3(tb.Lc, bf.B), dim3(B2G<LP>::THREADS), lds, s, tb, bf, gbuf, do_ab);
+}
+
+static int b2_check(const BlkTables &tb) {
+    if ((tb.log2p != 13 && tb.log2p != 14) || tb.Mc != 2 << tb.log2p || tb.Mr > (1 << tb.log2p) / 16)
+        return fail(SG_ERR_UNSUPPORTED, "block engine (two classes): P=2^%d, Mc=%d, Mr=%d", tb.log2p, tb.Mc, tb.Mr);
+    return SG_OK;
 }
 
 int blk2_launch_ab(const BlkTables &tb, const AmpBufs<float> &bf, hipStream_t s) {
     if (bf.B <= 0) return SG_OK;
-    if (tb.Mc != 2 * B2_P || tb.Mr > B2_THREADS)
-        return fail(SG_ERR_UNSUPPORTED, "block engine (two classes): Mc=%d, Mr=%d", tb.Mc, tb.Mr);
-    const size_t lds = blk2_lds_bytes();
+    SG_TRY(b2_check(tb));
+    const size_t lds = blk2_lds_bytes(tb.log2p);
     int rc = SG_OK;
     ProfScope ps(SG_PH_AB_A, s);
-    B2_EPS_DISPATCH(tb.M, b2_launch_ab, tb, bf, lds, s, &rc);
+    if (tb.log2p == 13) {
+        B2_EPS_DISPATCH(13, tb.M, b2_launch_ab, tb, bf, lds, s, &rc);
+    } else {
+        B2_EPS_DISPATCH(14, tb.M, b2_launch_ab, tb, bf, lds, s, &rc);
+    }
     SG_TRY(rc);
     SG_HIP(hipGetLastError());
     return SG_OK;
@@ -325,12 +356,16 @@ int blk2_launch_ab(const BlkTables &tb, const AmpBufs<float> &bf, hipStream_t s)
 
 int blk2_launch_az(const BlkTables &tb, const AmpBufs<float> &bf, cx<float> *gbuf, bool then_ab, hipStream_t s) {
     if (bf.B <= 0) return SG_OK;
-    if (tb.Mc != 2 * B2_P) return fail(SG_ERR_UNSUPPORTED, "block engine (two classes): Mc=%d", tb.Mc);
+    SG_TRY(b2_check(tb));
     SG_TRY(blk_launch_g(tb, bf, gbuf, s));
-    const size_t lds = blk2_lds_bytes();
+    const size_t lds = blk2_lds_bytes(tb.log2p);
     int rc = SG_OK;
     ProfScope ps(SG_PH_AZ_B, s);
-    B2_EPS_DISPATCH(tb.M, b2_launch_az, tb, bf, (const cx<float> *)gbuf, then_ab ? 1 : 0, lds, s, &rc);
+    if (tb.log2p == 13) {
+        B2_EPS_DISPATCH(13, tb.M, b2_launch_az, tb, bf, (const cx<float> *)gbuf, then_ab ? 1 : 0, lds, s, &rc);
+    } else {
+        B2_EPS_DISPATCH(14, tb.M, b2_launch_az, tb, bf, (const cx<float> *)gbuf, then_ab ? 1 : 0, lds, s, &rc);
+    }
     SG_TRY(rc);
     SG_HIP(hipGetLastError());
     return SG_OK;

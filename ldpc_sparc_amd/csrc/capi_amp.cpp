@@ -84,7 +84,8 @@ struct sg_amp_plan {
     void *c_gc = nullptr, *c_stw = nullptr;
     // block engine (several transforms per column block, amp_block.hip)
     bool block = false;
-    bool block2 = false;         // two-class block engine (w = 2^16, amp_block2.hip)
+    bool block2 = false;         // two-class block engine (amp_block2.hip): w = 2^16, or w = 2^15 in two
+    int b2_log2p = 0;            // classes of 2^13 points (two workgroups per CU); class size P = 2^b2_log2p
     int32_t *b_gk = nullptr;
     uint16_t *b_gloc = nullptr;
     uint32_t *b_pos2 = nullptr, *b_oab = nullptr;
@@ -289,6 +290,7 @@ static BlkTables btables(const sg_amp_plan *p) {
     tb.gk = p->b_gk;
     tb.stw = (const cx<float> *)p->b_stw;
     tb.skip = diag_skip();
+    tb.log2p = p->b2_log2p;
     return tb;
 }
 
@@ -1039,16 +1041,19 @@ static int build_block(sg_amp_plan *p, const uint32_t *order0, const uint32_t *o
     return SG_OK;
 }
 
-// Tables of the two-class block engine (amp_block2.hip): w = 2^16, N2 = 2 P with
-// P = 2^14.  Column entry j sits at packed slot m = 2 m1 + m2 of its transform:
-// class m2, real LDS index 2 fsw(m1) + component in the class image; owned by
-// (thread, entry) as b2_j.  Output coefficients per class fold the class
-// factor w_N2^(m2 k) and the last radix-4 stage: al = c1 w_N2^((m2 + 2 r) a).
+// Tables of the two-class block engine (amp_block2.hip): N2 = 2 P with P = 2^14
+// (w = 2^16) or 2^13 (w = 2^15).  Column entry j sits at packed slot
+// m = 2 m1 + m2 of its transform: class m2, real LDS index 2 ppos(m1) +
+// component in the class image; owned by (thread, entry) as b2_j.  Output
+// coefficients per class fold the class factor w_N2^(m2 k) and the last
+// radix-RF stage (RF = P / 4096): al = c1 w_N2^((m2 + 2 r) a).
 static int build_block2(sg_amp_plan *p, const uint32_t *order0, const uint32_t *order1,
                         const std::vector<double> &t_scale, const std::vector<int32_t> &row_of) {
     const long long N = p->w, N2 = p->N2;
     const int nT = p->nT, Mc = p->Mc, Mr = p->Mr, M = p->M;
-    constexpr int J = 32, T = 1024;
+    const int LP = p->b2_log2p, T = (1 << LP) / 16, RF = (1 << LP) / 4096;  // amp_block2.hip B2G
+    constexpr int J = 32;
+    SG_CHECK_ARG((LP == 13 || LP == 14) && N2 == 2LL << LP && Mc == 2 << LP, "internal: two-class geometry");
     // per (transform, class): the real LDS index 2 ppos(m1) + component of each column entry of the class in
     // the padded image, the trash slot (a padding slot, amp_block2.hip B2_TRASH) for the other class's entries
     constexpr uint32_t TRASH = 2 * 32;
@@ -1078,7 +1083,7 @@ static int build_block2(sg_amp_plan *p, const uint32_t *order0, const uint32_t *
             fwd_coef(o0[i], N, N2, t_scale[t], &a, &b, &c1, &c2);
             oab[(size_t)t * Mr + i] = (uint32_t)(a % 4096) | ((uint32_t)(b % 4096) << 16);
             for (int m2 = 0; m2 < 2; ++m2)
-                for (int r = 0; r < 4; ++r) {
+                for (int r = 0; r < RF; ++r) {  // (the last radix-RF stage folded in; RF = 2 leaves 4 zeros)
                     cd *o = &oc[(((size_t)t * 2 + m2) * Mr + i) * 8];
                     o[r] = c1 * tw((long long)(m2 + 2 * r) * a, N2);
                     o[4 + r] = c2 * std::conj(tw((long long)(m2 + 2 * r) * b, N2));
@@ -1102,7 +1107,7 @@ static int build_block2(sg_amp_plan *p, const uint32_t *order0, const uint32_t *
                           // sine / cosine stages of amp_block2.hip)
     {
         int radix[8];
-        const int ns = fft1_plan(14, 16, radix);
+        const int ns = fft1_plan(LP, 16, radix);
         int lns = 0;
         for (int st = 0; st < ns; ++st) {
             const int R = radix[st];
@@ -1123,7 +1128,7 @@ static int build_block2(sg_amp_plan *p, const uint32_t *order0, const uint32_t *
     SG_TRY(upload(p, &p->b_gi, gi));
     SG_TRY(upload_cx(p, &p->b_gc, gc));
     SG_TRY(upload_cx(p, &p->b_stw, stw));
-    SG_CHECK_ARG(blk2_lds_bytes() <= 160 * 1024, "block engine LDS budget");
+    SG_CHECK_ARG(blk2_lds_bytes(LP) <= 160 * 1024, "block engine LDS budget");
     return SG_OK;
 }
 
@@ -1190,12 +1195,19 @@ static int build_plan(int ndim, const double *W, int Lr_in, int Lc_in, int L, in
     p->regular = ndim <= 1 && p->nT == Lc && sec_bytes <= 32 * 1024 && !(eng && std::strcmp(eng, "legacy") == 0);
     // several transforms per column block, each small enough for one
     // workgroup's LDS: the block engine (single precision, w = 2^15)
-    p->block = !p->regular && precision == SG_F32 && p->N2 == (1 << 14) && Mc == (1 << 14) && M >= 64 &&
-               M <= 1024 && Mr < 65536 && !(eng && (std::strcmp(eng, "legacy") == 0 || std::strcmp(eng, "general") == 0));
-    // w = 2^16 with Mc = 2^15 (the notebook geometry): the two-class form
-    p->block2 = !p->regular && !p->block && precision == SG_F32 && p->N2 == (1 << 15) && Mc == (1 << 15) &&
-                M >= 64 && M <= 2048 && Mr <= 1024 &&
-                !(eng && (std::strcmp(eng, "legacy") == 0 || std::strcmp(eng, "general") == 0));
+    const bool no_blk = eng && (std::strcmp(eng, "legacy") == 0 || std::strcmp(eng, "general") == 0);
+    // w = 2^15 with Mc = 2^14 (C4): the single-class engine (one 1024-thread workgroup per CU, 132 KB of LDS);
+    // SG_AMP_BLOCK=two-class selects the two-class form at P = 2^13 (two 512-thread workgroups per CU), which
+    // measured no faster (block engine)
+    const char *bk = std::getenv("SG_AMP_BLOCK");
+    const bool single = !(bk && std::strcmp(bk, "two-class") == 0);
+    const bool c4 = !p->regular && precision == SG_F32 && p->N2 == (1 << 14) && Mc == (1 << 14) && M >= 64 && !no_blk;
+    p->block = c4 && single && M <= 1024 && Mr < 65536;
+    // w = 2^16 with Mc = 2^15 (the notebook geometry): the two-class form at P = 2^14
+    const bool nb = !p->regular && precision == SG_F32 && p->N2 == (1 << 15) && Mc == (1 << 15) && M >= 64 &&
+                    M <= 2048 && Mr <= 1024 && !no_blk;
+    p->block2 = (c4 && !single && M <= 2048 && Mr <= 512) || nb;
+    p->b2_log2p = p->block2 ? (nb ? 14 : 13) : 0;
     const int N = w, N2 = p->N2, P = p->P, Q = p->Q, np1 = p->npairs + 1;
     auto slot_of = [&](long long pos) -> long long {  // w-space slot of position pos
         return (pos % 2 == 0) ? pos / 2 : (long long)N - 1 - (pos - 1) / 2;

@@ -264,6 +264,26 @@ def test_c4_block_engine_vs_general_engine(monkeypatch):
     assert np.mean(mb != true) < 0.05  # the decode wave runs through at R = 1.5
 
 
+def test_c4_two_class_form_vs_single_class(monkeypatch):
+    """C4 through the two-class block engine at P = 2^13 (amp_block2.hip, two
+    512-thread workgroups per CU; SG_AMP_BLOCK=two-class) against the default
+    single-class engine (amp_block.hip) on the same batch: stopping iterations
+    within one, decisions and the first NMSE values agree (f32)."""
+    W, L, M, n, o0, o1 = _c4_design(7)
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    Y, true = _c4_batch(op, 8, 9)
+    monkeypatch.delenv("SG_AMP_BLOCK", raising=False)
+    m1, t1, n1, _ = sparc.amp_decode_batch(Y, op, 1.0, 40, true_idx=true, precision=_native.SG_F32)
+    monkeypatch.setenv("SG_AMP_BLOCK", "two-class")
+    o2 = sparc.DesignOperator(W, L, M, n, o0, o1)
+    m2, t2, n2, _ = sparc.amp_decode_batch(Y, o2, 1.0, 40, true_idx=true, precision=_native.SG_F32)
+    assert _native.amp_last_decode(o2.plan(_native.SG_F32))["engine"] == 3
+    assert np.all(np.abs(t1 - t2) <= 1)
+    assert np.mean(m1 != m2) < 1e-3
+    np.testing.assert_allclose(n1[:, :10], n2[:, :10], atol=1e-4)
+    assert np.mean(m2 != true) < 0.05
+
+
 def _notebook_design(seed):
     """The notebook's own geometry (sparc_demo_sc_decode_wave.ipynb cell 1):
     spatially coupled omega=6, Lambda=32, L=2048, M=512, R=1.5, P=15 ->

@@ -81,16 +81,20 @@ def windows(path, counter, engine_prefix):
         if r["Counter_Name"] == counter:
             name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("sg::", "")
             rows.append((int(r["Dispatch_Id"]), name, float(r["Counter_Value"])))
-    ids = [i for i, n, _ in rows if n.startswith((engine_prefix + "ab", engine_prefix + "az"))]
+    ab, az = engine_prefix
+    ids = [i for i, n, _ in rows if n.startswith(ab + az)]
     if not ids:
         return 0.0, 0
     lo, hi = min(ids), max(ids)
     tot = sum(v for i, _, v in rows if lo <= i <= hi)
-    naz = len({i for i, n, _ in rows if n.startswith(engine_prefix + "az")})
+    naz = len({i for i, n, _ in rows if n.startswith(az)})
     return tot, naz
 
 
-for key, prefix in (("sc", "blk_"), ("sc_notebook", "blk2_")):
+# (Ab, Az) kernel-name prefixes of each line's engine: C4 runs the two-class engine at P = 2^13
+# (blk2_*<13, M/64>; the single-class blk_* under SG_AMP_BLOCK=single), the notebook at P = 2^14
+for key, prefix in (("sc", (("blk_ab", "blk2_ab<13"), ("blk_az", "blk2_az<13"))),
+                    ("sc_notebook", (("blk2_ab<14",), ("blk2_az<14",)))):
     line = bench.get(key)
     if not line or not line.get("roofline", {}).get("launches"):
         continue
@@ -101,7 +105,8 @@ for key, prefix in (("sc", "blk_"), ("sc_notebook", "blk2_")):
     decodes = naz / az_per_decode if az_per_decode else 0
     units = decodes * line["batch_per_gpu"] * line["avg_iterations"]
     b = 2.0 * fb * 1024 + wb * 1024
-    out[key] = {"engine_kernels": prefix + "*", "decodes_in_window": decodes, "codeword_iterations": units,
+    out[key] = {"engine_kernels": "|".join(prefix[0] + prefix[1]), "decodes_in_window": decodes,
+                "codeword_iterations": units,
                 "hbm_bytes_per_codeword_iteration": b / units if units else None,
                 "note": "FETCH x2 + WRITE of every dispatch from the first to the last block-engine dispatch "
                         "(decodes incl. control kernels), over the executed codeword-iterations"}
