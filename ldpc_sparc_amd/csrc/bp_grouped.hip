@@ -43,15 +43,19 @@ __device__ __forceinline__ lds_f32 *ldsf(uint32_t byte) { return (lds_f32 *)(siz
 // global port table (gtab = the lane's entry; the table is L1-resident and
 // shared by the CU's workgroups, so the LDS holds only the messages), then the
 // reference's sum in port order and the extrinsic write-backs.
-template <int D>
-__device__ __forceinline__ float grp_var(const uint16_t *gtab, float acc) {
+// F2: first2 holds the slot addresses of the first two ports (low, high half)
+// in a register for the whole decode, so a degree-2 group reads no table at
+// all (the <4, 2> kernel; at <8, 4> the eight registers would spill)
+template <int D, bool F2>
+__device__ __forceinline__ float grp_var(const uint16_t *gtab, float acc, uint32_t first2) {
     if constexpr (D == 0) {
         return acc;
     } else {
         uint32_t sl[D];
         float m[D];
 #pragma unroll
-        for (int k = 0; k < D; ++k) sl[k] = gtab[64 * k];
+        for (int k = 0; k < D; ++k)
+            sl[k] = (F2 && k == 0) ? (first2 & 0xffffu) : (F2 && k == 1) ? (first2 >> 16) : (uint32_t)gtab[64 * k];
 #pragma unroll
         for (int k = 0; k < D; ++k) m[k] = *ldsf(sl[k]);
 #pragma unroll
@@ -92,9 +96,10 @@ __device__ __forceinline__ uint32_t grp_check(uint32_t addr, float factor, uint3
 }
 
 // uniform (per-wave) degree dispatch
-__device__ __forceinline__ float grp_var_d(int d, const uint16_t *gtab, float acc) {
+template <bool F2>
+__device__ __forceinline__ float grp_var_d(int d, const uint16_t *gtab, float acc, uint32_t first2) {
     switch (d) {
-#define SG_GV(N) case N: return grp_var<N>(gtab, acc);
+#define SG_GV(N) case N: return grp_var<N, F2>(gtab, acc, first2);
         SG_GV(0) SG_GV(1) SG_GV(2) SG_GV(3) SG_GV(4) SG_GV(5) SG_GV(6) SG_GV(7) SG_GV(8)
         SG_GV(9) SG_GV(10) SG_GV(11) SG_GV(12) SG_GV(13) SG_GV(14) SG_GV(15) SG_GV(16)
 #undef SG_GV
@@ -145,6 +150,15 @@ __global__ __launch_bounds__(BP_THREADS, VJ <= 4 ? 8 : 6) void bp_grouped_minsum
         cn[q] = __builtin_amdgcn_readfirstlane(mc[2 * GRP_WAVES * CJ + q]);
     }
     const int32_t *vmap = a.vmap + wave * VJ * 64 + lane;
+    constexpr bool F2 = VJ <= 4;
+    uint32_t first2[VJ];  // slot addresses of each variable group's first two ports (grp_var)
+#pragma unroll
+    for (int j = 0; j < VJ; ++j) {
+        const uint16_t *gt = a.vtab + vt[j] + lane;
+        first2[j] = !F2 ? 0u
+                        : (j < a.vj && vd[j] >= 1 ? (uint32_t)gt[0] : 0u) |
+                              (j < a.vj && vd[j] >= 2 ? (uint32_t)gt[64] << 16 : 0u);
+    }
     const float factor = a.factor;
     const uint32_t fsign = __float_as_uint(factor) & 0x80000000u;
     const int nwords = a.msg_bytes / 4;
@@ -164,7 +178,7 @@ __global__ __launch_bounds__(BP_THREADS, VJ <= 4 ? 8 : 6) void bp_grouped_minsum
             // ---- variable pass (c_ldpc.c:171-178)
 #pragma unroll
             for (int j = 0; j < VJ; ++j)
-                if (j < a.vj) apv[j] = grp_var_d(vd[j], a.vtab + vt[j] + lane, chv[j]);
+                if (j < a.vj) apv[j] = grp_var_d<F2>(vd[j], a.vtab + vt[j] + lane, chv[j], first2[j]);
             __syncthreads();
             // ---- check pass (c_ldpc.c:183-194 with the min-sum update)
             uint32_t unsat = 0u;
