@@ -45,6 +45,11 @@ constexpr int C2_SC = 9;   // class entries per thread and chunk
 constexpr int C2_NC = 2;   // chunks: a class holds at most C2_SC * C2_NC * 512 = 9216 entries
 static_assert(C2_EPT == 16, "the transform is written for 16 values per thread");
 
+// exp(x / tau) as exp2(x * (log2 e / tau)): __expf lowers to a multiply by log2 e and v_exp_f32, so
+// with log2 e folded into the per-codeword scale every exponential is one instruction
+constexpr double C2_LOG2E = 1.4426950408889634074;
+__device__ __forceinline__ float c2_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ int c2_opaque(int v) {
     asm volatile("" : "+v"(v));
     return v;
@@ -325,7 +330,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
     for (int l = tid; l < tb.L; l += C2_T) {  // previous beta's section max, 1/sum
         sMI[l] = c2f{bf.stM[lb + l], bf.stI[lb + l]};
     }
-    const float inv_tp = (float)(1.0 / bf.tau[cw]);
+    const float inv_tp = (float)(C2_LOG2E / bf.tau[cw]);  // log2 e / tau (c2_exp2)
     float *s = bf.s + (size_t)cw * tb.LM;  // s in; beta out (read by cw2_az, which writes the new s)
     cx<float> Ha[OT], Hb[OT];  // H[a], conj H[b] of the thread's outputs over this half's classes
 #pragma unroll
@@ -401,7 +406,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
             for (int i = c * C2_SC; i < (c + 1) * C2_SC; ++i) {
                 const int sec = e[i] >> 16;
                 const c2f mi = sMI[sec];
-                v[i] = __expf((v[i] - mi.x) * inv_tp) * mi.y;
+                v[i] = c2_exp2((v[i] - mi.x) * inv_tp) * mi.y;
                 dr[e[i] & 0xffffu] = v[i];
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[i]), rs, 4 * tl + 4 * i * C2_T,
                                                       0, 0);
@@ -525,7 +530,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
     const size_t lb = (size_t)cw * tb.L;
     const bool have_beta = t > 0;
     const double tv = bf.tau[cw];
-    const float tau = (float)tv, inv_tau = (float)(1.0 / tv);
+    const float tau = (float)tv, inv_tau = (float)(C2_LOG2E / tv);  // log2 e / tau (c2_exp2)
     float *s = bf.s + (size_t)cw * tb.LM;
     const float *vz = tb.vz + (size_t)cw * OT * C2_T;
     // running statistics of sections tid and tid + 512 over this half's classes
@@ -685,7 +690,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
             float S1 = 0.f, S2 = 0.f;
 #pragma unroll
             for (int i = 0; i < RC; ++i) {
-                float ex = __expf((x[i] - m) * inv_tau);
+                float ex = c2_exp2((x[i] - m) * inv_tau);
                 ex = i != am ? ex : 0.f;
                 S1 += ex;
                 S2 += ex * ex;
@@ -696,7 +701,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
                 for (int i = 0; i < RC; ++i) y[i] = dr[a + c + i];
 #pragma unroll
                 for (int i = 0; i < RC; ++i) {
-                    float ex = __expf((y[i] - m) * inv_tau);
+                    float ex = c2_exp2((y[i] - m) * inv_tau);
                     ex = (c + i < n && c + i != am) ? ex : 0.f;
                     S1 += ex;
                     S2 += ex * ex;
@@ -704,12 +709,12 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
             }
             if (m > -INFINITY) {  // merge into the section's running statistics
                 if (m > Mr[k]) {
-                    const float f = __expf((Mr[k] - m) * inv_tau);
+                    const float f = c2_exp2((Mr[k] - m) * inv_tau);
                     R1[k] = (R1[k] + 1.f) * f + S1;
                     R2[k] = (R2[k] + 1.f) * (f * f) + S2;
                     Mr[k] = m;
                 } else {
-                    const float f = __expf((m - Mr[k]) * inv_tau);
+                    const float f = c2_exp2((m - Mr[k]) * inv_tau);
                     R1[k] += (1.f + S1) * f;
                     R2[k] += (1.f + S2) * (f * f);
                 }
@@ -737,7 +742,7 @@ __global__ __launch_bounds__(1024) void cw2_merge(Cw2Tables tb, RegBufs<float> b
     if (!bf.active[cw]) return;
     const size_t lb = (size_t)cw * tb.L;
     const int Lb = tb.Lblk;
-    const float inv_tau = (float)(1.0 / bf.tau[cw]);
+    const float inv_tau = (float)(C2_LOG2E / bf.tau[cw]);  // log2 e / tau (c2_exp2)
     double a = 0.0, er = 0.0;
     if (tid < Lb) {
         const float4 *part = tb.part + (size_t)cw * 2 * Lb;
@@ -748,12 +753,12 @@ __global__ __launch_bounds__(1024) void cw2_merge(Cw2Tables tb, RegBufs<float> b
             if (!(p.w != p.w)) s_true = p.w;
             if (m > -INFINITY) {
                 if (m > Mr) {
-                    const float f = __expf((Mr - m) * inv_tau);
+                    const float f = c2_exp2((Mr - m) * inv_tau);
                     R1 = (R1 + 1.f) * f + p.y;
                     R2 = (R2 + 1.f) * (f * f) + p.z;
                     Mr = m;
                 } else {
-                    const float f = __expf((m - Mr) * inv_tau);
+                    const float f = c2_exp2((m - Mr) * inv_tau);
                     R1 += (1.f + p.y) * f;
                     R2 += (1.f + p.z) * (f * f);
                 }
@@ -769,7 +774,7 @@ __global__ __launch_bounds__(1024) void cw2_merge(Cw2Tables tb, RegBufs<float> b
             if (s_true == Mr) {
                 er = (r1 * r1 + r2) * i2;
             } else {
-                const double bt = (double)(__expf((s_true - Mr) * inv_tau) * inv);
+                const double bt = (double)(c2_exp2((s_true - Mr) * inv_tau) * inv);
                 er = (1.0 + r2) * i2 - 2.0 * bt + 1.0;
             }
         }
