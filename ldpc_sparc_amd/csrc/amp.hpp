@@ -225,6 +225,8 @@ struct Cw2Tables {
     const uint2 *wab;         // [OT][512] LDS byte addresses of the slot's row writes (rows r, P - r on the
                               // pair's last slot, else the trash slot; r = 0, P / 2: row r and trash)
     float *vz;                // [B][OT][512] z / phi in slot order
+    float *ys, *zs;           // [B][OT][512] y (copied at t = 0) and z in slot order (cw2_ctrl reads them
+                              // coalesced; z in natural order is still written for a hand-over)
     float4 *part;             // [B][2][Lblk] partial section statistics (max, R1, R2, s of the true entry or NaN)
     uint64_t *tprof;          // diagnostics (SG_AMP_TPROF): [2 B][64] shader-clock stamps (Ab 0-31, Az 32-63), or null
 };

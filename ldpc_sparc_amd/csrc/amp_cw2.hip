@@ -480,11 +480,21 @@ __global__ __launch_bounds__(C2_T) void cw2_ctrl(Cw2Tables tb, RegBufs<float> bf
     {
         int oi[OT];
         float yv[OT], zv[OT];
+        float *ys = tb.ys + (size_t)cw * OT * C2_T, *zs = tb.zs + (size_t)cw * OT * C2_T;
 #pragma unroll
         for (int j = 0; j < OT; ++j) {  // every load issued together (invalid slots: output 0, unused)
             oi[j] = tb.oi[j * C2_T + tid];
-            yv[j] = y[oi[j]];
-            zv[j] = have_beta ? z[oi[j]] : 0.f;
+            if (have_beta) {  // y and the previous z in slot order: one coalesced round trip
+                yv[j] = ys[j * C2_T + tid];
+                zv[j] = zs[j * C2_T + tid];
+            } else {  // first iteration: gather y and keep it in slot order
+                yv[j] = y[oi[j]];
+                zv[j] = 0.f;
+            }
+        }
+        if (!have_beta) {
+#pragma unroll
+            for (int j = 0; j < OT; ++j) ys[j * C2_T + tid] = yv[j];
         }
 #pragma unroll
         for (int j = 0; j < OT; ++j) {
@@ -497,8 +507,9 @@ __global__ __launch_bounds__(C2_T) void cw2_ctrl(Cw2Tables tb, RegBufs<float> bf
         }
 #pragma unroll
         for (int j = 0; j < OT; ++j) {
+            zs[j * C2_T + tid] = zr[j];
             if (tb.ka[j * C2_T + tid] & CW_VALID) {
-                z[oi[j]] = zr[j];
+                z[oi[j]] = zr[j];  // (natural order: the staged engine's after a hand-over)
                 if (sum_z) acc += (double)zr[j] * (double)zr[j];
             }
         }

@@ -78,7 +78,7 @@ struct sg_amp_plan {
     int32_t *c2_oi = nullptr;
     uint32_t *c2_wab = nullptr, *c2_rab = nullptr;
     void *c2_cf = nullptr, *c2_gf = nullptr;
-    void *ws_c2xp = nullptr, *ws_c2vz = nullptr, *ws_c2part = nullptr;
+    void *ws_c2xp = nullptr, *ws_c2vz = nullptr, *ws_c2part = nullptr, *ws_c2ys = nullptr, *ws_c2zs = nullptr;
     uint16_t *c_cmask = nullptr;  // [Q + 1][1024] per-codeword engine: written image values per thread
     int32_t *c_oa = nullptr, *c_ob = nullptr, *c_gi = nullptr;
     void *c_gc = nullptr, *c_stw = nullptr;
@@ -186,7 +186,7 @@ static int plan_free_ws(sg_amp_plan *p) {
                    (void **)&p->ws_psi, (void **)&p->ws_psi_prev, (void **)&p->ws_phi_prev, (void **)&p->ws_gamma,
                    (void **)&p->ws_bco, (void **)&p->ws_nmse, (void **)&p->ws_active, (void **)&p->ws_argmax,
                    (void **)&p->ws_true, (void **)&p->ws_tfinal, &p->ws_s, &p->ws_tu, &p->ws_xn, &p->ws_part,
-                   &p->ws_stM, &p->ws_stI, (void **)&p->ws_tau_prev, &p->ws_gbuf, &p->ws_c2xp, &p->ws_c2vz,
+                   &p->ws_stM, &p->ws_stI, (void **)&p->ws_tau_prev, &p->ws_gbuf, &p->ws_c2xp, &p->ws_c2vz, &p->ws_c2ys, &p->ws_c2zs,
                    &p->ws_c2part};
     for (void **x : ws) {
         if (*x) hipFree(*x);
@@ -221,6 +221,8 @@ static int ensure_ws(sg_amp_plan *p, int B, int t_max) {
         if (p->cw2OT) {
             SG_ALLOC(p->ws_c2xp, Bz * 2 * p->cw2OT * CW2_THREADS * 4);
             SG_ALLOC(p->ws_c2vz, Bz * p->cw2OT * CW2_THREADS * 4);
+            SG_ALLOC(p->ws_c2ys, Bz * p->cw2OT * CW2_THREADS * 4);
+            SG_ALLOC(p->ws_c2zs, Bz * p->cw2OT * CW2_THREADS * 4);
             SG_ALLOC(p->ws_c2part, Bz * 2 * p->Lblk * 16);
         }
         SG_ALLOC(p->ws_stM, Bz * p->L * rs);
@@ -906,7 +908,7 @@ static Cw2Tables c2tables(const sg_amp_plan *p) {
     tb.cmask = p->c2_cmask; tb.ka = p->c2_ka; tb.oi = p->c2_oi;
     tb.cf = (const float4 *)p->c2_cf; tb.gf = (const float4 *)p->c2_gf;
     tb.cls_ptr = p->r_cls_ptr; tb.cls_ls = p->r_cls_ls; tb.cls2 = p->c2_cls; tb.qpos = p->r_qpos; tb.seg = p->r_seg;
-    tb.xr = (float *)p->ws_c2xp; tb.vz = (float *)p->ws_c2vz; tb.wab = (const uint2 *)p->c2_wab; tb.rab = (const uint2 *)p->c2_rab; tb.part = (float4 *)p->ws_c2part;
+    tb.xr = (float *)p->ws_c2xp; tb.vz = (float *)p->ws_c2vz; tb.ys = (float *)p->ws_c2ys; tb.zs = (float *)p->ws_c2zs; tb.wab = (const uint2 *)p->c2_wab; tb.rab = (const uint2 *)p->c2_rab; tb.part = (float4 *)p->ws_c2part;
     tb.tprof = p->tprof;  // [2 B][64] stamps (the buffer holds B * Q * 20 >= 128 B words)
     return tb;
 }
