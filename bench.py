@@ -251,7 +251,7 @@ class HostCounterComm:
         pass
 
 
-PMC_TRAFFIC_FILES = ("r03_pmc_traffic_bench_v4.json", "r03_pmc_traffic_bench_v2.json", "r03_pmc_traffic_bench.json", "r02_pmc_traffic_bench.json", "r01_pmc_traffic_bench.json")
+PMC_TRAFFIC_FILES = ("r03_pmc_traffic_bench_v5.json", "r03_pmc_traffic_bench_v4.json", "r03_pmc_traffic_bench_v2.json", "r03_pmc_traffic_bench.json", "r02_pmc_traffic_bench.json", "r01_pmc_traffic_bench.json")
 
 
 def pmc_traffic(section, field, kernel_prefix=None):
