@@ -141,19 +141,29 @@ __device__ __forceinline__ void b2_ab_column(const BlkTables &tb, const AmpBufs<
             __syncthreads();
 #pragma unroll
             for (int i = 0; i < B2_J; ++i) dr[b2_pos(pv, i)] = bv[i];  // (the other class's entries: trash slot)
+            // the output's bins and coefficients, requested before the transform (their L2 round trip
+            // hides behind it; requested after it, one workgroup per CU waited for it every class)
+            constexpr int RF = B2G<LP>::RF;
+            const bool own = tl < tb.Mr;
+            const int io = own ? tl : 0;
+            const uint32_t ab = tb.oab[(size_t)t * tb.Mr + io];
+            const cx<float> *oc = tb.oc + (((size_t)t * 2 + m2) * tb.Mr + io) * 8;
+            cx<float> al[RF], be[RF];
+#pragma unroll
+            for (int r = 0; r < RF; ++r) {
+                al[r] = oc[r];
+                be[r] = oc[4 + r];
+            }
             __syncthreads();
             b2_fwd_stages<LP>(d, tl);
             // X_i += Re(sum_r al_r Y[a mod 4096 + 4096 r] + be_r conj Y[b mod ...]), r < RF:
             // the last stage and w_N2^(m2 k) are in the coefficients
-            if (tl < tb.Mr) {
-                const uint32_t ab = tb.oab[(size_t)t * tb.Mr + tl];
+            if (own) {
                 const int ja = ab & 0xffffu, jb = ab >> 16;
-                const cx<float> *oc = tb.oc + (((size_t)t * 2 + m2) * tb.Mr + tl) * 8;
 #pragma unroll
-                for (int r = 0; r < B2G<LP>::RF; ++r) {  // ppos(j + 4096 r) = ppos(j) + 4224 r for j < 4096
+                for (int r = 0; r < RF; ++r) {  // ppos(j + 4096 r) = ppos(j) + 4224 r for j < 4096
                     const cx<float> ya = d[ppos(ja) + 4224 * r], yb = d[ppos(jb) + 4224 * r];
-                    const cx<float> al = oc[r], be = oc[4 + r];
-                    acc += (al.x * ya.x - al.y * ya.y) + (be.x * yb.x + be.y * yb.y);
+                    acc += (al[r].x * ya.x - al[r].y * ya.y) + (be[r].x * yb.x + be[r].y * yb.y);
                 }
             }
             __syncthreads();
