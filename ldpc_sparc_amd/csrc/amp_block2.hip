@@ -208,14 +208,21 @@ __global__ __launch_bounds__(B2G<LP>::THREADS, 4) void blk2_az(BlkTables tb, Amp
         const int g0 = tb.gptr[t], ng = tb.gptr[t + 1] - g0;
         for (int m2 = 0; m2 < 2; ++m2) {
             const int tl = b2_opaque(tid);
-            b2_clear<LP>(smem, tl);
-            __syncthreads();
             // rows of class m2: U[k1] = sum over k = k1 mod P of G[k] conj(w_N2^(m2 k));
             // at most two slots (k1, k1 + P) share a row, and two float additions
-            // onto a zero commute, so the atomic sum is deterministic
-            for (int g = tl; g < ng; g += T) {
-                const int k = tb.gk[g0 + g];
-                cx<float> v = gcw[g0 + g];
+            // onto a zero commute, so the atomic sum is deterministic.  The thread's
+            // first two slots are requested before the clear (in flight during it).
+            int kp[2];
+            cx<float> vp[2];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int g = tl + e * T < ng ? tl + e * T : 0;
+                kp[e] = tb.gk[g0 + g];
+                vp[e] = gcw[g0 + g];
+            }
+            b2_clear<LP>(smem, tl);
+            __syncthreads();
+            auto row = [&](int k, cx<float> v) {
                 if (m2) {
                     const float x = (float)k * inv_n2;  // conj(w_N2^k) = exp(+2 pi i k / N2)
                     const float cs = __builtin_amdgcn_cosf(x), sn = __builtin_amdgcn_sinf(x);
@@ -224,7 +231,11 @@ __global__ __launch_bounds__(B2G<LP>::THREADS, 4) void blk2_az(BlkTables tb, Amp
                 cx<float> *dst = &d[ppos(k & (P - 1))];
                 atomicAdd(&dst->x, v.x);
                 atomicAdd(&dst->y, v.y);
-            }
+            };
+#pragma unroll
+            for (int e = 0; e < 2; ++e)
+                if (tl + e * T < ng) row(kp[e], vp[e]);
+            for (int g = tl + 2 * T; g < ng; g += T) row(tb.gk[g0 + g], gcw[g0 + g]);
             __syncthreads();
             // (stage twiddles from the hardware sine / cosine: no table entries in flight, u[] stays in registers)
             lds_fft1_sincos<true, 16, LP, 0, 4, true>(d, tl);
