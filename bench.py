@@ -17,7 +17,10 @@ coupled, block engine) in the "sc" object, C5 (concatenated SPARC+LDPC) in
 Roofline: the AMP kernels of one iteration against HBM with SURVEY.md 8(d)'s
 algorithmic bytes per codeword-iteration 4*(2LM+4n); the BP kernel with
 4*(4*Nmsg+N) bytes per codeword-iteration.  Kernel durations come from HIP
-events recorded on the library stream around every launch in the timed region.
+events recorded on the library stream in the timed region: around every AMP
+iteration of the C2 line (its four kernels; an event between two kernels holds
+the second back, so the per-kernel split is taken from the last warmup step),
+around every launch elsewhere.
 
 Roofline: the C2 headline leads with the binding bound, the f32 vector ALUs
 (SURVEY.md 8(d) flops per codeword-iteration; the FFTs run on the VALU), with
