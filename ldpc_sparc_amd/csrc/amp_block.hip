@@ -91,20 +91,25 @@ __device__ __forceinline__ void bk_pos_load(const BlkTables &tb, int t, int tid,
 __device__ __forceinline__ uint32_t bk_pos(const uint32_t *pv, int i) { return (pv[i >> 1] >> (16 * (i & 1))) & 0xffffu; }
 
 // The first three stages of the 2^14-point FFT of fft.hpp (radix 16, 16, 16,
-// then 4; stage twiddles from the hardware sine / cosine): the forward
-// transform stops before the radix-4 stage, which Ab folds into the
-// needed outputs.
-__device__ __forceinline__ void bk_fwd_stages(cx<float> *d, const cx<float> *__restrict__ stw, int tid) {
+// then 4): the forward transform stops before the radix-4 stage, which Ab
+// folds into the needed outputs.  Stages 0-1 and stage 2 separately, so that
+// the outputs' table entries can be requested in between (in flight during
+// the last stage; across all three stages they would spill).
+__device__ __forceinline__ void bk_fwd_stages01(cx<float> *d, const cx<float> *__restrict__ stw, int tid,
+                                                cx<float> *w2) {
     if constexpr (SG_BLK_SINCOS & 1) {
-        lds_fft1_sincos<false, 16, BK_LOG2N, 0, 3, true>(d, tid);
+        lds_fft1_sincos<false, 16, BK_LOG2N, 0, 2, true>(d, tid);
     } else {
-        cx<float> w0[1], w1[6], w2[6];
+        cx<float> w0[1], w1[6];
         fft1_tw_load_ct<float, 16, BK_LOG2N, 1>(stw, tid, w1);
         stockham1_stage_ct<float, false, 16, 16, BK_LOG2N, 0, true>(d, w0, tid);
         fft1_tw_load_ct<float, 16, BK_LOG2N, 2>(stw, tid, w2);
         stockham1_stage_ct<float, false, 16, 16, BK_LOG2N, 4, true>(d, w1, tid);
-        stockham1_stage_ct<float, false, 16, 16, BK_LOG2N, 8, true>(d, w2, tid);
     }
+}
+__device__ __forceinline__ void bk_fwd_stage2(cx<float> *d, int tid, const cx<float> *w2) {
+    if constexpr (SG_BLK_SINCOS & 1) lds_fft1_sincos<false, 16, BK_LOG2N, 2, 3, true>(d, tid);
+    else stockham1_stage_ct<float, false, 16, 16, BK_LOG2N, 8, true>(d, w2, tid);
 }
 
 // ------------------------------------------------------------------ Ab
@@ -126,14 +131,37 @@ __device__ __forceinline__ void bk_ab_column(const BlkTables &tb, const AmpBufs<
         for (int i = 0; i < BK_J; ++i)
             dr[bk_pos(pv, i)] = bv[i];
         __syncthreads();
-        bk_fwd_stages(d, tb.stw, tl);
+        cx<float> w2[6];
+        bk_fwd_stages01(d, tb.stw, tl, w2);
         // the last (radix-4, Ns = 4096) stage only for the needed bins, folded
         // into the outputs: H[a] = sum_r Y[a mod 4096 + 4096 r] w_N2^(r a), so
         // X_i = Re(c1 H[a] + c2 conj H[b]) = Re(sum_r al_r Y_a,r + be_r conj Y_b,r)
         float *r = bf.rbuf + ((size_t)cw * tb.nT + t) * tb.Mr;
         const uint32_t *oab = tb.oab + (size_t)t * tb.Mr;
         const cx<float> *oc = tb.oc + (size_t)t * tb.Mr * 8;
-        for (int i = tl; i < tb.Mr; i += BK_THREADS) {
+        {  // the thread's first output: its entries requested before the last stage
+            const bool own = tl < tb.Mr;
+            const int io = own ? tl : 0;
+            const uint32_t ab = oab[io];
+            cx<float> al[4], be[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                al[q] = oc[8 * io + q];
+                be[q] = oc[8 * io + 4 + q];
+            }
+            bk_fwd_stage2(d, tl, w2);
+            if (own) {
+                const int ja = ab & 0xffffu, jb = ab >> 16;
+                float acc = 0.f;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {  // ppos(j + 4096 q) = ppos(j) + 4224 q for j < 4096
+                    const cx<float> ya = d[ppos(ja) + 4224 * q], yb = d[ppos(jb) + 4224 * q];
+                    acc += (al[q].x * ya.x - al[q].y * ya.y) + (be[q].x * yb.x + be[q].y * yb.y);
+                }
+                r[tl] = acc;
+            }
+        }
+        for (int i = tl + BK_THREADS; i < tb.Mr; i += BK_THREADS) {  // (Mr > 1024 only)
             const uint32_t ab = oab[i];
             const int ja = ab & 0xffffu, jb = ab >> 16;
             float acc = 0.f;
