@@ -73,3 +73,19 @@ def test_split_engine_first_iterations_track(monkeypatch):
         pa = _decode(monkeypatch, op, Y, true, True, tm)[3][:, 0]
         pb = _decode(monkeypatch, op, Y, true, False, tm)[3][:, 0]
         np.testing.assert_allclose(pa, pb, rtol=2e-6)
+
+
+def test_profile_levels_split_engine(monkeypatch):
+    """sg_profile_enable(2) (bench.py's timed region) records the split
+    engine's per-iteration scope only; level 1 also records its kernels.  The
+    decode itself is the same either way."""
+    op, true, Y = _batch(1024, 512, 1.5, 256, 41, 5)
+    out = {}
+    for level in (1, 2):
+        prof = _native.Profiler(level)
+        m, t, n, _ = _decode(monkeypatch, op, Y, true, True, t_max=4)
+        out[level] = (prof.stop(), m, t)
+    ph1, ph2 = out[1][0], out[2][0]
+    assert ph1["amp_iter"][1] == ph2["amp_iter"][1] == 3  # t_max - 1 iterations
+    assert ph1["cw2_az"][1] == 3 and "cw2_az" not in ph2 and "cw2_ab" not in ph2
+    assert np.array_equal(out[1][1], out[2][1]) and np.array_equal(out[1][2], out[2][2])
