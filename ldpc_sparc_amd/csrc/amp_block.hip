@@ -291,14 +291,16 @@ __global__ __launch_bounds__(BK_THREADS) void blk_az(BlkTables tb, AmpBufs<float
     const int lane = tid & 63, wv = tid >> 6;
     constexpr int eps = EPS, spw = 1024 / (64 * EPS);
     const int nsec = tb.Mc / tb.M;
-    const float tau = (float)bf.tau[(size_t)cw * tb.Lc + c], itau = 1.0f / tau;
+    // x = s log2(e) / tau (sparc.py:430 in base 2: exp(s / tau - max) = exp2(x - max x), one v_exp_f32;
+    // __expf is a multiply by log2 e and v_exp_f32), the reciprocal once (IEEE division is ~10 VALU)
+    const float tau = (float)bf.tau[(size_t)cw * tb.Lc + c], itau = (float)(1.4426950408889634074 / (double)tau);
     float *beta = bf.beta + (size_t)cw * tb.LM + (size_t)c * tb.Mc;
     float s[BK_J], x[BK_J], bv[BK_J];
 #pragma unroll
     for (int i = 0; i < BK_J; ++i) {
         const int j = bk_j<EPS>(tid, i);
         s[i] = beta[j] + tau * u[i];  // sparc.py:972
-        x[i] = s[i] * itau;           // sparc.py:430 (reciprocal once: IEEE division is ~10 VALU)
+        x[i] = s[i] * itau;           // sparc.py:430, scaled by log2 e
     }
     const int l0 = c * nsec;  // first section of the column block
 #pragma unroll
@@ -322,7 +324,7 @@ __global__ __launch_bounds__(BK_THREADS) void blk_az(BlkTables tb, AmpBufs<float
         float dn = 0.f;
 #pragma unroll
         for (int e = 0; e < eps; ++e) {
-            x[i0 + e] = __expf(x[i0 + e] - xm);
+            x[i0 + e] = __builtin_amdgcn_exp2f(x[i0 + e] - xm);
             dn += x[i0 + e];
         }
         dn = bk_wave_sum(dn);

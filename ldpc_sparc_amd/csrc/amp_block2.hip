@@ -253,7 +253,9 @@ __global__ __launch_bounds__(B2G<LP>::THREADS, 4) void blk2_az(BlkTables tb, Amp
     const int lane = tid & 63, wv = tid >> 6;
     constexpr int eps = EPS, spw = 2048 / (64 * EPS);
     const int nsec = tb.Mc / tb.M;
-    const float tau = (float)bf.tau[(size_t)cw * tb.Lc + c], itau = 1.0f / tau;
+    // x = s log2(e) / tau (sparc.py:430 in base 2: exp(s / tau - max) = exp2(x - max x), one v_exp_f32;
+    // __expf is a multiply by log2 e and v_exp_f32), the reciprocal once (IEEE division is ~10 VALU)
+    const float tau = (float)bf.tau[(size_t)cw * tb.Lc + c], itau = (float)(1.4426950408889634074 / (double)tau);
     float *beta = bf.beta + (size_t)cw * tb.LM + (size_t)c * tb.Mc;
     const int l0 = c * nsec;  // first section of the column block
     float bv[B2_J];  // the new beta_c, kept for the next iteration's Ab (do_ab)
@@ -265,7 +267,7 @@ __global__ __launch_bounds__(B2G<LP>::THREADS, 4) void blk2_az(BlkTables tb, Amp
 #pragma unroll
         for (int e = 0; e < eps; ++e) {
             s[e] = beta[ls * tb.M + lane * eps + e] + tau * u[i0 + e];  // sparc.py:972
-            x[e] = s[e] * itau;                                         // sparc.py:430
+            x[e] = s[e] * itau;                                         // sparc.py:430, scaled by log2 e
         }
         float xm = -INFINITY, sm = -INFINITY;
         int arg = 0x7fffffff;
@@ -283,7 +285,7 @@ __global__ __launch_bounds__(B2G<LP>::THREADS, 4) void blk2_az(BlkTables tb, Amp
         float dn = 0.f;
 #pragma unroll
         for (int e = 0; e < eps; ++e) {
-            x[e] = __expf(x[e] - xm);
+            x[e] = __builtin_amdgcn_exp2f(x[e] - xm);
             dn += x[e];
         }
         dn = b2_wave_sum(dn);
