@@ -113,6 +113,10 @@ int sg_dense_amp_iteration(sg_dense_plan *p, const double *y, const double *beta
  * sg_dense_amp_device call (valid until the next call; lets a pipeline feed
  * the glue without copies). */
 int sg_dense_state_device(sg_dense_plan *p, void **d_beta, void **d_s);
+/* Device pointer of the plan's design matrix A [n][L*M] (row-major, the
+ * plan's precision, no padding) -- lets a checker read A back in row blocks
+ * (tests/test_c5_full_gpu.py) without a second copy. */
+int sg_dense_plan_matrix_device(const sg_dense_plan *p, const void **d_A);
 /* x = A beta0 for one-hot beta0 (section index d_idx [B][L], value sqrt(n P / L)). */
 int sg_dense_encode_device(sg_dense_plan *p, const int32_t *d_idx, int B, void *d_x, void *stream);
 /* MAP section indices of s [B][L*M] (msg_vector_map_estimator, sparc_new.py:1099-1116). */
@@ -173,7 +177,10 @@ int sg_ldpc_decode_kernel(const sg_graph *g, int dectype, int precision, char *n
  * double arithmetic; SG_F32 is the throughput path. */
 int sg_ldpc_decode(sg_graph *g, int dectype, int precision, const double *ch, int B, int max_it,
                    double corr, double *app, int32_t *it);
-/* Device variant: d_ch/d_app are float or double per `precision`. */
+/* Device variant: d_ch/d_app are float or double per `precision`.  SG_F32
+ * min-sum on a graph of the degree-grouped layout (bp_grouped.hip) expects
+ * NaN-free channel LLRs and saturates them at +-1e30; the host entry point
+ * above sends a batch holding a NaN to the table kernel instead. */
 int sg_ldpc_decode_device(sg_graph *g, int dectype, int precision, const void *d_ch, int B,
                           int max_it, double corr, void *d_app, int32_t *d_it, void *stream);
 /* Device-side error counting against known codewords (ldpc_awgn.py:97-104):

@@ -104,6 +104,7 @@ SIGNATURES = [
     ("sg_dense_encode_device", ct.c_int, [vp, vp, ct.c_int, vp, vp]),
     ("sg_dense_map_device", ct.c_int, [vp, vp, ct.c_int, vp, vp]),
     ("sg_dense_state_device", ct.c_int, [vp, ct.POINTER(vp), ct.POINTER(vp)]),
+    ("sg_dense_plan_matrix_device", ct.c_int, [vp, ct.POINTER(vp)]),
     ("sg_concat_count_errors_device", ct.c_int, [ct.c_int, vp, vp, ct.c_int, ct.c_int, ct.c_int, ct.c_int, vp, vp,
                                                  ct.c_int, ct.c_int, ct.c_int, vp, vp]),
     ("sg_beta_to_llr_device", ct.c_int, [ct.c_int, vp, ct.c_int, ct.c_int, ct.c_int, ct.c_double, ct.c_int,

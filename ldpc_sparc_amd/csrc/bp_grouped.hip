@@ -25,11 +25,20 @@
 //     LDS address by 256 B, one add per port).
 // Per group and pass one table load (vector L1) and two LDS round trips;
 // 2 VALU per variable port, ~7 per check port.  Built with -fno-honor-nans: no NaN reaches the min/max (the
-// channel LLRs are finite and the messages are sums and products of them), so
-// the compiler drops the canonicalisation of their operands.
+// channel LLRs are saturated to finite values on load, GRP_CH_MAX, and the
+// messages are sums and products of them), so the compiler drops the
+// canonicalisation of their operands.  A NaN channel LLR is outside the
+// kernel's contract: the host entry point sends such a batch to the table
+// kernel (capi_ldpc.cpp), the device entry point documents it.
 #include "bp.hpp"
 
 namespace sg {
+
+// Channel LLRs are saturated at this magnitude on load (far beyond any LLR a
+// channel produces: 2y / sigma^2 ~ 1e30 needs |y| / sigma^2 ~ 5e29).  Up to 17
+// terms of it still sum to a finite float, so no inf - inf reaches the
+// variable pass from the input.
+constexpr float GRP_CH_MAX = 1e30f;
 
 // LDS words addressed by their byte address.  The kernel has no static LDS
 // (grouped_one checks), so its dynamic image starts at address 0 and the
@@ -168,7 +177,9 @@ __global__ __launch_bounds__(BP_THREADS, VJ <= 4 ? 8 : 6) void bp_grouped_minsum
 #pragma unroll
         for (int j = 0; j < VJ; ++j) {
             const int v = j < a.vj ? vmap[64 * j] : -1;
-            chv[j] = v >= 0 ? ch[v] : 0.0f;
+            // saturated at +-GRP_CH_MAX (and inf with it): the kernel is built
+            // without NaN semantics, and a sum of saturated inputs stays finite
+            chv[j] = v >= 0 ? __builtin_amdgcn_fmed3f(ch[v], -GRP_CH_MAX, GRP_CH_MAX) : 0.0f;
             apv[j] = 0.0f;
         }
         for (int i = tid; i < nwords; i += BP_THREADS) reinterpret_cast<float *>(smem)[i] = 0.0f;

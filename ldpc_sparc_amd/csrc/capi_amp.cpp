@@ -885,7 +885,7 @@ static RegTables<T> rtables(const sg_amp_plan *p) {
     return tb;
 }
 
-static CwTables ctables(const sg_amp_plan *p) {
+static CwTables ctables(const sg_amp_plan *p, int B) {
     CwTables tb;
     tb.L = p->L; tb.M = p->M; tb.LM = p->LM; tb.n = p->n; tb.N2 = p->N2; tb.Q = p->rQ; tb.Lblk = p->Lblk;
     tb.KT = p->cwKT; tb.log2P = p->rlog2P; tb.maxcls = p->rmaxcls; tb.maxseg = p->rmaxseg;
@@ -896,11 +896,12 @@ static CwTables ctables(const sg_amp_plan *p) {
     tb.cls_ptr = p->r_cls_ptr; tb.cls_ls = p->r_cls_ls; tb.qpos = p->r_qpos; tb.seg = p->r_seg;
     tb.stw = (const cx<float> *)p->c_stw;
     tb.inv_n2 = 1.0f / (float)p->N2;
-    tb.tprof = p->tprof;  // [B][32] stamps (the buffer holds B * Q * 20 >= 32 B words)
+    // [B][32] stamps, only when the diagnostics buffer holds them
+    tb.tprof = (p->tprof && p->tprof_items * 20 >= (size_t)32 * B) ? p->tprof : nullptr;
     return tb;
 }
 
-static Cw2Tables c2tables(const sg_amp_plan *p) {
+static Cw2Tables c2tables(const sg_amp_plan *p, int B) {
     Cw2Tables tb;
     tb.L = p->L; tb.M = p->M; tb.LM = p->LM; tb.n = p->n; tb.N2 = p->N2; tb.Q = p->rQ; tb.Lblk = p->Lblk;
     tb.OT = p->cw2OT; tb.maxcls = p->rmaxcls;
@@ -909,7 +910,9 @@ static Cw2Tables c2tables(const sg_amp_plan *p) {
     tb.cf = (const float4 *)p->c2_cf; tb.gf = (const float4 *)p->c2_gf;
     tb.cls_ptr = p->r_cls_ptr; tb.cls_ls = p->r_cls_ls; tb.cls2 = p->c2_cls; tb.qpos = p->r_qpos; tb.seg = p->r_seg;
     tb.xr = (float *)p->ws_c2xp; tb.vz = (float *)p->ws_c2vz; tb.ys = (float *)p->ws_c2ys; tb.zs = (float *)p->ws_c2zs; tb.wab = (const uint2 *)p->c2_wab; tb.rab = (const uint2 *)p->c2_rab; tb.part = (float4 *)p->ws_c2part;
-    tb.tprof = p->tprof;  // [2 B][64] stamps (the buffer holds B * Q * 20 >= 128 B words)
+    // [2 B][64] stamps, only when the diagnostics buffer holds them (build_cw2
+    // accepts any even Q, and B * Q * 20 < 128 B for Q < 7)
+    tb.tprof = (p->tprof && p->tprof_items * 20 >= (size_t)128 * B) ? p->tprof : nullptr;
     return tb;
 }
 
@@ -1397,8 +1400,8 @@ static int decode_regular(sg_amp_plan *p, const void *d_y, int B, const int32_t 
     for (int t = 0; t < t_max - 1; ++t) {
         if constexpr (std::is_same<T, float>::value) {
             if (cw) {
-                if (use_cw2(p)) SG_TRY(cw2_launch_iter(c2tables(p), bf, sc, pr, t, s));
-                else SG_TRY(cw_launch_iter(ctables(p), bf, sc, pr, t, s));
+                if (use_cw2(p)) SG_TRY(cw2_launch_iter(c2tables(p, B), bf, sc, pr, t, s));
+                else SG_TRY(cw_launch_iter(ctables(p, B), bf, sc, pr, t, s));
             }
         }
         if (!cw) {

@@ -507,6 +507,12 @@ int sg_dense_state_device(sg_dense_plan *p, void **d_beta, void **d_s) {
     return SG_OK;
 }
 
+int sg_dense_plan_matrix_device(const sg_dense_plan *p, const void **d_A) {
+    SG_CHECK_ARG(p && d_A, "null argument");
+    *d_A = p->A;
+    return SG_OK;
+}
+
 int sg_dense_map_device(sg_dense_plan *p, const void *d_s, int B, int32_t *d_idx, void *stream) {
     SG_CHECK_ARG(p && d_s && d_idx, "null argument");
     if (B <= 0) return SG_OK;

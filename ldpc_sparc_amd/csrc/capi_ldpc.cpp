@@ -58,6 +58,10 @@ static bool build_groups(sg_graph *g, const int64_t *vdeg, const int64_t *cdeg, 
                          const std::vector<int32_t> &voff, const std::vector<int32_t> &coff, hipStream_t s) {
     const int nv = g->nv, nc = g->nc;
     if (g->max_cdeg > GRP_MAXDC || g->max_vdeg > GRP_MAXDV) return false;
+    // the per-degree check code covers degrees 2..8 only (grp_check_d): a
+    // check of degree 0 or 1 takes the table kernel
+    for (int c = 0; c < nc; ++c)
+        if (cdeg[c] < 2) return false;
     // checks by degree (descending, stable), groups of 64 of one degree
     std::vector<int> corder(nc);
     for (int c = 0; c < nc; ++c) corder[c] = c;
@@ -243,7 +247,7 @@ static bool use_grouped() {
 }
 
 static int decode_device(sg_graph *g, int dectype, int precision, const void *d_ch, int B, int max_it,
-                         double corr, void *d_app, int32_t *d_it, hipStream_t s) {
+                         double corr, void *d_app, int32_t *d_it, hipStream_t s, bool ch_has_nan = false) {
     SG_CHECK_ARG(g, "graph is NULL");
     SG_CHECK_ARG(B >= 0, "negative batch");
     SG_CHECK_ARG(dectype == SG_SUMPROD || dectype == SG_SUMPROD2 || dectype == SG_MINSUM,
@@ -258,7 +262,7 @@ static int decode_device(sg_graph *g, int dectype, int precision, const void *d_
         SG_HIP(hipStreamSynchronize(s));
         return SG_OK;
     }
-    if (precision == SG_F32 && dectype == SG_MINSUM && g->grp_ok && use_grouped()) {
+    if (precision == SG_F32 && dectype == SG_MINSUM && g->grp_ok && use_grouped() && !ch_has_nan) {
         BpGrpArgs a;
         a.meta = g->d_grp_meta; a.vmap = g->d_grp_vmap; a.vtab = g->d_grp_vtab;
         a.ntab = g->grp_ntab; a.msg_bytes = g->grp_msg_bytes; a.vj = g->grp_vj; a.cj = g->grp_cj;
@@ -301,15 +305,21 @@ static int decode_host(sg_graph *g, int dectype, int precision, const double *ch
     SG_TRY(ensure_staging(g, B));
     hipStream_t s = lib_stream();
     const size_t n = (size_t)B * g->nv;
+    bool ch_has_nan = false;
     if (precision == SG_F64) {
         SG_HIP(hipMemcpyAsync(g->d_ch, ch, n * sizeof(double), hipMemcpyHostToDevice, s));
     } else {
         std::vector<float> tmp(n);
-        for (size_t i = 0; i < n; ++i) tmp[i] = (float)ch[i];
+        bool nan = false;
+        for (size_t i = 0; i < n; ++i) {
+            tmp[i] = (float)ch[i];
+            nan |= std::isnan(ch[i]);
+        }
+        ch_has_nan = nan;  // a NaN input goes to the table kernel (NaN semantics)
         SG_HIP(hipMemcpyAsync(g->d_ch, tmp.data(), n * sizeof(float), hipMemcpyHostToDevice, s));
         SG_HIP(hipStreamSynchronize(s));
     }
-    SG_TRY(decode_device(g, dectype, precision, g->d_ch, B, max_it, corr, g->d_app, g->d_it, s));
+    SG_TRY(decode_device(g, dectype, precision, g->d_ch, B, max_it, corr, g->d_app, g->d_it, s, ch_has_nan));
     SG_HIP(hipMemcpyAsync(it, g->d_it, sizeof(int32_t) * B, hipMemcpyDeviceToHost, s));
     if (precision == SG_F64) {
         SG_HIP(hipMemcpyAsync(app, g->d_app, n * sizeof(double), hipMemcpyDeviceToHost, s));

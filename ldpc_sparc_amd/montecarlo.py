@@ -72,6 +72,12 @@ def _first_reaching(cum, need):
     return int(hit[0]) if hit.size else None
 
 
+# Campaign parameters added to the checkpoints after round 3, with the value
+# an older checkpoint implies: such a checkpoint still resumes when the new
+# run uses that value (concat_ber_sweep's min_errors None).
+_LEGACY_PARAM_DEFAULTS = {"min_errors": None}
+
+
 def run_point(trial, point, *, block, blocks_per_round, rank, world, agg, min_errors=None, max_units=None,
               checkpoint_dir=None, tag="campaign", params=None, max_rounds=None):
     """Run one point until `min_errors` frame errors or `max_units` units
@@ -100,7 +106,11 @@ def run_point(trial, point, *, block, blocks_per_round, rank, world, agg, min_er
         if os.path.exists(path):
             with open(path) as f:
                 st = json.load(f)
-            if st.get("params") != json.loads(json.dumps(params)):
+            want = json.loads(json.dumps(params))
+            for k, v in _LEGACY_PARAM_DEFAULTS.items():  # checkpoints written before the key existed
+                if k not in st.get("params", {}) and want.get(k, v) == v:
+                    want.pop(k, None)
+            if st.get("params") != want:
                 raise ValueError(f"checkpoint {path} was written with parameters {st.get('params')}, "
                                  f"not {params}: use another checkpoint_dir or tag")
             total = np.array(st["counts"], dtype=np.int64)
@@ -325,7 +335,9 @@ def concat_ber_sweep(L, M, n, P, L_unprotected, mults, ebn0_db, *, codewords, bl
     the bench: awgn_var = P / (2 R_overall 10^(Eb/N0 / 10)), R_overall = user
     bits / n.  Returns one dict per point; rank 0 writes `npz_file` in the
     layout of performance_plots_general.py:138 (ber_store_averages, _max,
-    _min over the blocks rank 0 decoded, and snr_store = Eb/N0 in dB).
+    _min over the blocks rank 0 decoded, and snr_store = Eb/N0 in dB), plus a
+    `complete` flag per point; a sweep that `max_rounds` interrupted writes
+    `<npz_file>.partial.npz` instead, so it never overwrites a final file.
     `trial(point, first_block, n_blocks, block)` (counters as ConcatTrial's)
     replaces the GPU pipeline (CPU rehearsals: tools/c5_sweep.py --rehearsal); `max_rounds`
     interrupts every point after that many rounds (run_point); `on_point(dict)`
@@ -361,14 +373,20 @@ def concat_ber_sweep(L, M, n, P, L_unprotected, mults, ebn0_db, *, codewords, bl
                     "ber": float(tot[1]) / (tot[0] * user_bits) if tot[0] else None,
                     "fer": float(tot[2]) / tot[0] if tot[0] else None,
                     "unprotected_bit_errors": int(tot[3]), "protected_bit_errors": int(tot[4]),
-                    "R_overall": r_overall})
+                    "R_overall": r_overall,
+                    # False when max_rounds interrupted the point before its target
+                    "complete": bool(tot[0] >= codewords or (min_errors is not None and tot[2] >= min_errors))})
         if on_point is not None:
             on_point(out[-1])
     if npz_file and rank == 0:
+        complete = np.array([o["complete"] for o in out])
+        if not complete.all():  # an interrupted sweep never overwrites a final file
+            npz_file = (npz_file[:-4] if npz_file.endswith(".npz") else npz_file) + ".partial.npz"
         avg = np.array([[o["ber"] for o in out]], dtype=float)
         bb = [getattr(trial, "block_ber", {}).get(p, [np.nan]) for p in range(len(ebn0_db))]
         np.savez(npz_file, ber_store_averages=avg, ber_store_max=np.array([[np.max(b) for b in bb]]),
-                 ber_store_min=np.array([[np.min(b) for b in bb]]), snr_store=np.asarray(ebn0_db, dtype=float))
+                 ber_store_min=np.array([[np.min(b) for b in bb]]), snr_store=np.asarray(ebn0_db, dtype=float),
+                 complete=complete)
     return out
 
 

@@ -120,3 +120,57 @@ def test_graphs_outside_the_grouped_layout_take_the_table_kernel():
             assert _kernel(g, "sumprod2", _native.SG_F64).startswith("bp_flood_kernel<double, 1,")
         finally:
             _native.lib().sg_ldpc_graph_destroy(g)
+    # a degree-1 check (the per-degree check code covers 2..8)
+    vdeg, cdeg, intrlv = _random_graph((2, 3), 200, rng, 8)
+    k = int(np.argmax(cdeg >= 3))
+    cdeg = np.concatenate([cdeg[:k], [1, cdeg[k] - 1], cdeg[k + 1:]]).astype(np.int64)
+    g = _graph(vdeg, cdeg, intrlv)
+    try:
+        assert _kernel(g).startswith("bp_flood_kernel<float, 2,"), _kernel(g)
+    finally:
+        _native.lib().sg_ldpc_graph_destroy(g)
+
+
+def test_nan_channel_input_takes_the_table_kernel(monkeypatch):
+    """The grouped kernel has no NaN semantics (built -fno-honor-nans): a host
+    batch holding a NaN decodes through the table kernel, so its results equal
+    the table kernel's."""
+    c = code("802.11n", "1/2", 27)
+    ch = _awgn(c, 1.5, 8, np.random.default_rng(4))
+    ch[3, 17] = np.nan
+    vdeg, cdeg, intrlv = (np.asarray(a, np.int64) for a in (c.vdeg, c.cdeg, c.intrlv))
+    g = _graph(vdeg, cdeg, intrlv)
+    try:
+        monkeypatch.setenv("SG_BP_GROUPED", "1")
+        app, it = _decode(g, ch, 20, 0.7)
+        monkeypatch.setenv("SG_BP_GROUPED", "0")
+        tapp, tit = _decode(g, ch, 20, 0.7)
+        assert np.array_equal(it, tit) and np.array_equal(app.view(np.uint32), tapp.view(np.uint32))
+    finally:
+        _native.lib().sg_ldpc_graph_destroy(g)
+
+
+@pytest.mark.parametrize("ebn0", [1.0, 2.0])
+def test_c3_batch_every_workgroup_decodes_several_codewords(monkeypatch, ebn0):
+    """C3 at its bench size (B = 4096, BASELINE.json configs[2]): the grouped
+    kernel's grid is 4 workgroups per CU (bp_grouped.hip:228), so each
+    workgroup decodes B / grid codewords in turn, reusing its LDS image and its
+    parity-buffered stop flags.  Bit for bit against the float32 restatement of
+    the corrected min-sum (c_ldpc.c:339-381) at iteration caps 1 and 50."""
+    c = code("802.11n", "1/2", 81)
+    B = 4096
+    assert B > 4 * _native.cu_count()
+    ch = _awgn(c, ebn0, B, np.random.default_rng(int(ebn0 * 10) + 3))
+    vdeg, cdeg, intrlv = (np.asarray(a, np.int64) for a in (c.vdeg, c.cdeg, c.intrlv))
+    g = _graph(vdeg, cdeg, intrlv)
+    try:
+        assert _kernel(g).startswith("bp_grouped_minsum_kernel<4, 2>"), _kernel(g)
+        monkeypatch.setenv("SG_BP_GROUPED", "1")
+        ch32 = ch.astype(np.float32).astype(np.float64)
+        for mi in (1, 50):
+            app, it = _decode(g, ch32, mi, 0.7)
+            rapp, rit = bp.minsum_numpy(ch32, vdeg, cdeg, intrlv, mi, 0.7, np.float32)
+            assert np.array_equal(it, rit), mi
+            assert np.array_equal(app.view(np.uint32), rapp.view(np.uint32)), mi
+    finally:
+        _native.lib().sg_ldpc_graph_destroy(g)

@@ -215,3 +215,36 @@ def test_c5_sweep_rehearsal_world8_kill_and_resume(tmp_path):
     assert all(p["codewords"] <= 2 * 8 * 256 for p in part[:-1])
     # the error target ends the low-Eb/N0 points early; the high ones run to the codeword cap
     assert full[0]["codewords"] < 40960 and full[-2]["codewords"] == 40960
+
+
+def test_checkpoint_without_min_errors_key_resumes(tmp_path):
+    """A checkpoint written before min_errors was recorded (round 3) resumes
+    a run whose min_errors is None, the value it implies; another value is
+    still refused."""
+    d = str(tmp_path)
+    mc.run_point(fake_trial, 0, block=64, blocks_per_round=5, rank=0, world=1, agg=mc.Aggregator(),
+                 max_units=640, checkpoint_dir=d, params={"seed": 1}, max_rounds=1)
+    path = mc._ckpt_path(d, "campaign", 0)
+    st = json.load(open(path))
+    assert "min_errors" not in st["params"]
+    tot = mc.run_point(fake_trial, 0, block=64, blocks_per_round=5, rank=0, world=1, agg=mc.Aggregator(),
+                       max_units=640, checkpoint_dir=d, params={"seed": 1, "min_errors": None})
+    assert tot[0] == 640
+    with pytest.raises(ValueError):
+        mc.run_point(fake_trial, 0, block=64, blocks_per_round=5, rank=0, world=1, agg=mc.Aggregator(),
+                     max_units=640, checkpoint_dir=d, params={"seed": 1, "min_errors": 10})
+
+
+def test_interrupted_sweep_writes_partial_npz(tmp_path):
+    """concat_ber_sweep with max_rounds: the per-point dicts say complete=False
+    and the arrays go to <npz>.partial.npz, never over the final file."""
+    import numpy as np
+    npz = str(tmp_path / "c5.npz")
+    kw = dict(codewords=4096, block=256, blocks_per_round=2, trial=lambda p, a, n, b: np.array(
+        [n * b, 3 * n, n, 2 * n, n], dtype=np.int64), npz_file=npz)
+    part = mc.concat_ber_sweep(1024, 512, 9216, 15.0, 160, 4, [5.0, 6.0], max_rounds=1, **kw)
+    assert not any(p["complete"] for p in part)
+    assert os.path.exists(str(tmp_path / "c5.partial.npz")) and not os.path.exists(npz)
+    full = mc.concat_ber_sweep(1024, 512, 9216, 15.0, 160, 4, [5.0, 6.0], **kw)
+    assert all(p["complete"] for p in full)
+    assert np.load(npz)["complete"].all()
