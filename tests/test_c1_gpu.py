@@ -92,4 +92,6 @@ def test_c1_f32_matrix_cores(c1):
         assert np.array_equal(idx[clear], ref_idx[clear]), k
         bits = ((idx[:, None] >> np.arange(9)[::-1]) & 1).ravel()
         ber = np.mean(bits != c1[f"c1_s{k}_bits_in"])
+        print(f"  seed {k}: {int(clear.sum())} of {L} sections clear, BER {ber:.4f} vs {float(c1[f'c1_s{k}_ber']):.4f}",
+              flush=True)
         assert abs(ber - float(c1[f"c1_s{k}_ber"])) < 0.02, (k, ber)
