@@ -57,6 +57,12 @@ from ldpc_sparc_amd.ldpc import code  # noqa: E402
 METRIC = "codewords/sec (AMP+BP) at L=1024 M=512 / n=1944; BER match vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 VALU_PEAK_TFS = 157.3  # MI355X f32 vector peak (packed FMA), MI355X_MICROARCH.md
+# FP64 vector peak: MI355X_MICROARCH.md has no FP64 row.  v_fma_f64 issues at half the f32 packed-FMA
+# rate on CDNA3/CDNA4 (MI300X: 81.7 vs 163.4 TF), i.e. 157.3 / 2 = 78.6 TF, AMD's MI355X figure; the
+# dependent-FMA microbenchmark tools/fp64peak.hip measures it on the box (profiles/r04_fp64peak.txt).
+VALU_F64_PEAK_TFS = 78.65
+VALU_F64_PEAK_SOURCE = ("157.3 TF f32 vector peak (MI355X_MICROARCH.md) / 2: v_fma_f64 at half the packed-f32 "
+                        "FMA rate (AMD MI355X spec 78.6 TF FP64 vector); measured: profiles/r04_fp64peak.txt")
 AMP_PHASES = ("ab_passA", "ab_passB", "az_passA", "az_passB", "eta", "control", "amp_iter")
 
 
@@ -254,25 +260,54 @@ class HostCounterComm:
         pass
 
 
-PMC_TRAFFIC_FILES = ("r03_pmc_traffic_bench_v5.json", "r03_pmc_traffic_bench_v4.json", "r03_pmc_traffic_bench_v2.json", "r03_pmc_traffic_bench.json", "r02_pmc_traffic_bench.json", "r01_pmc_traffic_bench.json")
+def lib_digest():
+    """sha256 prefix of the library this process runs: PMC summaries carry the
+    digest of the build they were measured on (tools/pmc_bench.py,
+    tools/pmc_sq_bench.py), and the bench reports their bytes and instruction
+    counts only for that same build -- a kernel change that keeps its name can
+    never borrow an older build's counters."""
+    import hashlib
+    with open(_native.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def _pmc_file(kind):
+    """The newest profiles/*_pmc_{kind}_bench*.json measured on this build, or
+    (None, None)."""
+    import glob
+    dig = lib_digest()
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_{kind}_bench*.json")),
+                       key=os.path.getmtime, reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if d.get("lib_sha256") == dig:
+            return d, os.path.basename(path)
+    return None, None
 
 
 def pmc_traffic(section, field, kernel_prefix=None):
-    """HBM bytes per unit from the committed PMC passes of tools/pmc_bench.sh
-    over this bench (the newest profiles/rNN_pmc_traffic_bench.json that has
-    the section -- and, with kernel_prefix, was measured on that kernel, so an
-    older engine's traffic is never reported for a newer one): (value, file)
-    or (None, None)."""
-    for name in PMC_TRAFFIC_FILES:
-        try:
-            with open(os.path.join(REPO, "profiles", name)) as f:
-                sec = json.load(f)[section]
-            if kernel_prefix and not str(sec.get("kernel", "")).startswith(kernel_prefix):
-                continue
-            return sec[field], name
-        except (OSError, KeyError, ValueError):
-            continue
-    return None, None
+    """HBM bytes per unit from the PMC passes of tools/pmc_bench.sh over this
+    bench on this library build (FETCH_SIZE x2 + WRITE_SIZE): (value, file),
+    or (None, None) when no pass of this build is committed."""
+    d, name = _pmc_file("traffic")
+    try:
+        sec = d[section]
+        if kernel_prefix and not str(sec.get("kernel", "")).startswith(kernel_prefix):
+            return None, None
+        return sec[field], name
+    except (TypeError, KeyError):
+        return None, None
+
+
+def pmc_sq(section):
+    """SQ counter summary (tools/pmc_sq_bench.sh) of this build: (dict, file) or (None, None)."""
+    d, name = _pmc_file("sq")
+    if d is None or section not in d:
+        return None, None
+    return d[section], name
 
 
 # ------------------------------------------------------------------ AMP (C2)
@@ -359,21 +394,36 @@ def amp_f64(args, d, comm, cpu_seconds, procs, steps=2):
     st = amp_setup(a, d.rank)
     amp_step(st, a, comm)
     _native.device_synchronize()
+    prof = _native.Profiler()  # HIP events on the library stream around every kernel phase
     d.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
         amp_step(st, a, comm)
     _native.device_synchronize()
     el = d.max(time.perf_counter() - t0)
+    phases = prof.stop()
     cnt = st["d_cnt"].download(np.zeros(4, np.int64))
     tf = st["d_tf"].download(np.zeros(st["B"], np.int32))
+    amp_ms = sum(phases.get(p, (0.0, 0))[0] for p in AMP_PHASES)
+    cw_it = int(tf.sum()) * steps
+    w = int(st["op"].w)
+    flops_per_cwit = 2 * 2.5 * w * np.log2(w) + 20 * st["L"] * st["M"]
+    tfl = flops_per_cwit * cw_it / (amp_ms * 1e-3) / 1e12 if amp_ms > 0 else None
     out = {"workload": f"C2 in double precision: L=1024, M=512, n={st['n']}, R={args.rate}, t_max={args.t_max}, "
                        "same design and batch as the f32 line",
            "value": d.world * st["B"] * steps / el, "unit": "codewords/s", "dtype": "f64",
            "batch_per_gpu": st["B"], "steps": steps, "avg_iterations": float(tf.mean()),
            "engine": {1: "staged (amp_fused.hip)", 0: "general (amp_dct.hip)"}.get(
                _native.lib().sg_amp_plan_engine(st["plan"], st["B"]), "?"),
-           "section_errors": int(cnt[0]), "bit_errors": int(cnt[1]), "codeword_errors": int(cnt[2])}
+           "section_errors": int(cnt[0]), "bit_errors": int(cnt[1]), "codeword_errors": int(cnt[2]),
+           "roofline": {"bound": "valu-f64", "achieved": tfl, "peak": VALU_F64_PEAK_TFS, "unit": "TFLOP/s",
+                        "frac": tfl / VALU_F64_PEAK_TFS if tfl else None,
+                        "peak_source": VALU_F64_PEAK_SOURCE,
+                        "algorithmic_flops_per_codeword_iteration": flops_per_cwit, "codeword_iterations": cw_it,
+                        "kernel_ms": {k: round(v[0], 3) for k, v in phases.items()},
+                        "launches": {k: v[1] for k, v in phases.items()},
+                        "note": "same flop figure as the f32 line (SURVEY.md 8(d)) over the summed kernel time of "
+                                "the timed steps (HIP events around every kernel phase on the library stream)"}}
     if cpu_seconds > 0:
         out["cpu_baseline"] = amp_cpu_baseline(st, a, cpu_seconds, procs)
     return out
@@ -813,6 +863,14 @@ def main():
                       if engine == 2 else (None, None))
     cw_it_per_launch = cw_it / launches if launches else None
     tflops = flops_per_cwit * cw_it / (amp_ms * 1e-3) / 1e12 if amp_ms > 0 else None
+    # the two factors of the f32-peak fraction from the SQ passes over this build (tools/pmc_sq_bench.sh):
+    # VALU issue = wave64 VALU instructions x 4 cycles / (SIMDs x 2.4 GHz x kernel time), and algorithmic
+    # flops per VALU lane-instruction (4 at most: v_pk_fma_f32); frac = issue x flops-per-lane / 4
+    sq, sqfile = pmc_sq("amp") if (engine == 2 and split) else (None, None)
+    vpc = sq["valu_wave_insts_per_codeword_iteration"] if sq else None
+    ncu = _native.cu_count()
+    valu_issue = (vpc * cw_it * 4.0 / (4 * ncu * 2.4e9 * amp_ms * 1e-3)) if (vpc and amp_ms > 0) else None
+    flops_lane = flops_per_cwit / (64.0 * vpc) if vpc else None
     gbs = bytes_per_cwit * cw_it / (amp_ms * 1e-3) / 1e9 if amp_ms > 0 else None
     kernel = (("one AMP iteration of the batch = cw2_ab + cw2_ctrl + cw2_az + cw2_merge (four launches, "
                "amp_cw2.hip; 'launch' below = one iteration)") if (engine == 2 and split) else
@@ -844,9 +902,17 @@ def main():
         "roofline": {"bound": "valu-f32", "achieved": tflops, "peak": VALU_PEAK_TFS, "unit": "TFLOP/s",
                      "frac": tflops / VALU_PEAK_TFS if tflops else None,
                      "traffic": traffic * cw_it_per_launch if (traffic and cw_it_per_launch) else None,
-                     "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE + WRITE_SIZE per codeword-iteration, "
-                                     f"profiles/{tfile}, x codeword-iterations per launch)",
+                     "traffic_unit": ("HBM bytes per launch (PMC FETCH_SIZE + WRITE_SIZE per codeword-iteration, "
+                                      f"profiles/{tfile}, x codeword-iterations per launch)") if tfile else
+                                     "no PMC pass of this library build committed (traffic null)",
                      "traffic_per_codeword_iteration": traffic,
+                     "valu_issue_frac": valu_issue, "flops_per_lane_instr": flops_lane,
+                     "valu_wave_insts_per_codeword_iteration": vpc,
+                     "lds_bank_conflict_frac": sq.get("lds_bank_conflict_frac") if sq else None,
+                     "sq_file": sqfile, "lib_sha256": lib_digest(),
+                     "factor_note": "frac = valu_issue_frac x flops_per_lane_instr / 4 (SQ_INSTS_VALU of this "
+                                    "build's SQ passes; issue at the nominal 2.4 GHz); null when no SQ pass of "
+                                    "this build is committed",
                      "engine": engine_name, "kernel": kernel,
                      "algorithmic_flops_per_codeword_iteration": flops_per_cwit,
                      "codeword_iterations": cw_it, "codeword_iterations_per_launch": cw_it_per_launch,
@@ -916,7 +982,7 @@ def main():
                                   "note": "the messages never leave LDS: 16 Nmsg bytes of f32 message reads and "
                                           "writes per codeword-iteration against the LDS peak for that mix "
                                           "(ds_read_b32 128 B/clk/CU, ds_write_b32 64 B/clk/CU, harmonic mean, "
-                                          "2.4 GHz); SQ counters in profiles/r03_pmc_sq_bench.json"},
+                                          "2.4 GHz); SQ counters of this build: tools/pmc_sq_bench.sh"},
                      "roofline_hbm": {"bound": "hbm", "achieved_if_streamed": bach, "peak": HBM_PEAK_GBS,
                                       "unit": "GB/s", "algorithmic_bytes_per_codeword_iteration": bbytes,
                                       "traffic": hbm_meas,

@@ -17,7 +17,11 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // ------------------------------------------------------------------ f32 MFMA GEMM
 // C[M][N] (+)= X[M][K] . Y, X K-contiguous; Y = [N][K] (NT) or [K][N] (NN).
-// 128 x 128 x 32 block tile, 4 waves in 2 x 2, each 64 x 64 = 2 x 2 MFMA tiles.
+// (64 MT) x 128 x 32 block tile, 4 waves in 2 x 2, each (32 MT) x 64 = MT x 2
+// MFMA tiles.  MT = 4 covers a whole 256-codeword batch in one block row, so
+// the design matrix (the Y operand, 19 GB at C5) is read once per launch; MT =
+// 2 (128-row blocks) serves batches of at most 128.  Every output's k-order is
+// the same for both (one MFMA chain over its K chunk), so they agree bit for bit.
 struct GemmF32 {
     const float *X;
     long ldx;
@@ -30,28 +34,36 @@ struct GemmF32 {
     int M, N, K, kchunk, yrows;  // yrows: rows of Y (N for NT, K rows for NN) that exist
 };
 
-constexpr int GBM = 128, GBN = 128, GBK = 32, GPAD = GBK + 1;
+constexpr int GBN = 128, GBK = 32, GPAD = GBK + 1;
+template <int MT>
+constexpr int gbm() { return 64 * MT; }
 
-template <bool NT>
-__global__ __launch_bounds__(256) void gemm_f32_mfma(GemmF32 g) {
-    __shared__ float Xs[GBM * GPAD];
+template <bool NT, int MT>
+__global__ __launch_bounds__(256, MT == 4 ? 2 : 1) void gemm_f32_mfma(GemmF32 g) {  // (MT 4: 2 waves per SIMD)
+    constexpr int BM = gbm<MT>(), XL = BM / 32;  // float4 loads of the X tile per thread
+    __shared__ float Xs[BM * GPAD];
     __shared__ float Ys[NT ? GBN * GPAD : GBK * GBN];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid >> 1, wn = wid & 1;
-    const int m0 = blockIdx.y * GBM, n0 = blockIdx.x * GBN;
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * GBN;
     const int kb = blockIdx.z * g.kchunk;
     const int ke = min(g.K, kb + g.kchunk);
     const int nk = (ke - kb + GBK - 1) / GBK;
-    float4 xr[4], yr[4];
+    float4 xr[XL], yr[4];
     auto load = [&](int k0) {
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
+        for (int p = 0; p < XL; ++p) {
             const int f = tid + 256 * p;
             const int r = f >> 3, c = (f & 7) * 4;
             const int m = m0 + r;
             xr[p] = (m < g.M && k0 + c < ke) ? *reinterpret_cast<const float4 *>(g.X + (long)m * g.ldx + k0 + c)
                                              : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int f = tid + 256 * p;
             if (NT) {
+                const int r = f >> 3, c = (f & 7) * 4;
                 const int nn = n0 + r;
                 yr[p] = (nn < g.yrows && k0 + c < ke)
                             ? *reinterpret_cast<const float4 *>(g.Y + (long)nn * g.ldy + k0 + c)
@@ -65,9 +77,9 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma(GemmF32 g) {
             }
         }
     };
-    f32x16 acc[2][2];
+    f32x16 acc[MT][2];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < MT; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
@@ -76,12 +88,17 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma(GemmF32 g) {
     for (int kt = 0; kt < nk; ++kt) {
         __syncthreads();
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
+        for (int p = 0; p < XL; ++p) {
             const int f = tid + 256 * p;
             const int r = f >> 3, c = (f & 7) * 4;
             float *xd = Xs + r * GPAD + c;
             xd[0] = xr[p].x; xd[1] = xr[p].y; xd[2] = xr[p].z; xd[3] = xr[p].w;
+        }
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int f = tid + 256 * p;
             if (NT) {
+                const int r = f >> 3, c = (f & 7) * 4;
                 float *yd = Ys + r * GPAD + c;
                 yd[0] = yr[p].x; yd[1] = yr[p].y; yd[2] = yr[p].z; yd[3] = yr[p].w;
             } else {
@@ -94,15 +111,15 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma(GemmF32 g) {
 #pragma unroll
         for (int kk = 0; kk < GBK / 2; ++kk) {
             const int kx = 2 * kk + (lane >> 5);
-            float a[2], b[2];
+            float a[MT], b[2];
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt) a[mt] = Xs[(wm * 64 + mt * 32 + (lane & 31)) * GPAD + kx];
+            for (int mt = 0; mt < MT; ++mt) a[mt] = Xs[(wm * 32 * MT + mt * 32 + (lane & 31)) * GPAD + kx];
 #pragma unroll
             for (int nt = 0; nt < 2; ++nt)
                 b[nt] = NT ? Ys[(wn * 64 + nt * 32 + (lane & 31)) * GPAD + kx]
                            : Ys[kx * GBN + wn * 64 + nt * 32 + (lane & 31)];
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
+            for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
                 for (int nt = 0; nt < 2; ++nt)
                     acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
@@ -110,18 +127,28 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma(GemmF32 g) {
     }
     float *C = g.C + (long)blockIdx.z * g.c_split;
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int row = m0 + wm * 64 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                const int row = m0 + wm * 32 * MT + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
                 const int col = n0 + wn * 64 + nt * 32 + (lane & 31);
                 if (row < g.M && col < g.N) {
                     const long o = (long)row * g.ldc + col;
                     C[o] = g.add ? g.add[o] + acc[mt][nt][r] : acc[mt][nt][r];
                 }
             }
+}
+
+// Block rows of 256 once the batch exceeds 128 codewords (A read ceil(B / 256)
+// times instead of ceil(B / 128)); 128 below that (no idle half tile).
+template <bool NT>
+static void gemm_launch(const GemmF32 &g, unsigned gx, unsigned gz, hipStream_t s) {
+    if (g.M > gbm<2>())
+        hipLaunchKernelGGL((gemm_f32_mfma<NT, 4>), dim3(gx, (g.M + gbm<4>() - 1) / gbm<4>(), gz), dim3(256), 0, s, g);
+    else
+        hipLaunchKernelGGL((gemm_f32_mfma<NT, 2>), dim3(gx, (g.M + gbm<2>() - 1) / gbm<2>(), gz), dim3(256), 0, s, g);
 }
 
 // ------------------------------------------------------------------ f64 (parity) products
@@ -402,8 +429,7 @@ int dense_launch_ab<float>(const DenseBufs<float> &d, hipStream_t s) {
     g.X = d.beta; g.ldx = d.LM; g.Y = d.A; g.ldy = d.LM; g.C = d.part; g.ldc = d.n; g.add = nullptr;
     g.c_split = (long)d.B * d.n; g.M = d.B; g.N = d.n; g.K = d.LM; g.yrows = d.n;
     g.kchunk = ((d.LM + d.nsplit - 1) / d.nsplit + GBK - 1) / GBK * GBK;
-    hipLaunchKernelGGL(gemm_f32_mfma<true>, dim3((d.n + GBN - 1) / GBN, (d.B + GBM - 1) / GBM, d.nsplit), dim3(256),
-                       0, s, g);
+    gemm_launch<true>(g, (d.n + GBN - 1) / GBN, d.nsplit, s);
     SG_HIP(hipGetLastError());
     return SG_OK;
 }
@@ -421,8 +447,7 @@ int dense_launch_az<float>(const DenseBufs<float> &d, hipStream_t s) {
     GemmF32 g;
     g.X = d.z; g.ldx = d.npad; g.Y = d.A; g.ldy = d.LM; g.C = d.s; g.ldc = d.LM; g.add = d.beta;
     g.c_split = 0; g.M = d.B; g.N = d.LM; g.K = d.npad; g.kchunk = d.npad; g.yrows = d.n;
-    hipLaunchKernelGGL(gemm_f32_mfma<false>, dim3((d.LM + GBN - 1) / GBN, (d.B + GBM - 1) / GBM, 1), dim3(256), 0,
-                       s, g);
+    gemm_launch<false>(g, (d.LM + GBN - 1) / GBN, 1, s);
     SG_HIP(hipGetLastError());
     return SG_OK;
 }

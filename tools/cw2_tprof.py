@@ -34,9 +34,8 @@ out = np.zeros((items.value, 10), np.uint64)
 _native.check(lib.sg_amp_stage_raw(plan, 0, out.ctypes.data_as(ct.POINTER(ct.c_uint64)), ct.byref(items)))
 st = out[:, :8].reshape(-1)[:2 * B * 64].reshape(2 * B, 64).astype(np.int64)
 Qh = 32
-names = {(0, 1): "Ab: loads + scatter chunk 0", (1, 2): "Ab: scatter chunk 1", (2, 3): "Ab: barrier",
-         (3, 6): "Ab: FFT", (6, 8): "Ab: a loads + accumulate", (8, 9): "Ab: closing barrier",
-         (0, 9): "Ab: class total",
+names = {(0, 8): "Ab: loads + prev accumulate + barrier", (8, 1): "Ab: scatter chunk 0",
+         (1, 2): "Ab: scatter chunk 1", (2, 3): "Ab: barrier", (3, 6): "Ab: FFT", (0, 6): "Ab: class (to FFT end)",
          (32, 33): "Az: rows", (33, 34): "Az: barrier", (34, 35): "Az: FFT (inverse)", (35, 36): "Az: s_new",
          (36, 37): "Az: s store", (37, 38): "Az: barrier", (38, 39): "Az: class copy + barrier",
          (39, 40): "Az: section stats", (40, 41): "Az: closing barrier", (32, 41): "Az: class total"}

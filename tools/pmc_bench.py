@@ -9,8 +9,13 @@ usage: python tools/pmc_bench.py FETCH.csv WRITE.csv bench.json out.json
 tools/pmc_concat.sh adds its MFMA-busy fraction)"""
 import collections
 import csv
+import hashlib
 import json
+import os
 import sys
+
+LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ldpc_sparc_amd", "_lib",
+                   "libldpc_sparc_amd.so")
 
 
 def load(path, counter):
@@ -34,7 +39,8 @@ for k in sorted(set(fetch) | set(write)):
     d = max(nd.get(k, 1), 1)
     per[k] = {"dispatches": d, "read_bytes_per_dispatch": 2.0 * fetch.get(k, 0.0) * 1024 / d,
               "write_bytes_per_dispatch": write.get(k, 0.0) * 1024 / d}
-out = {"kernels": per, "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes; FETCH x2 (gfx950)"}
+out = {"kernels": per, "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes; FETCH x2 (gfx950)",
+       "lib_sha256": hashlib.sha256(open(LIB, "rb").read()).hexdigest()[:16]}  # the build these bytes belong to
 rf = bench.get("roofline", {})
 c2k = [n for n in per if n.startswith("cw2_")]
 cwk = next((n for n in per if n.startswith("cw_iter")), None)
