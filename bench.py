@@ -739,6 +739,7 @@ def concat_bench(args, d):
     el = d.max(time.perf_counter() - t0)
     ph = prof.stop()
     cnt = pipe.counts()
+    match = concat_decision_check(pipe, B, min(B, 16)) if args.cpu_seconds > 0 and d.rank == 0 else None
     gemm_ms = ph.get("dense_gemm", (0.0, 0))[0]
     concat_traffic, concat_tfile = pmc_traffic("concat", "hbm_bytes_per_gemm_launch")
     concat_mfma, _ = pmc_traffic("concat", "mfma_busy_frac")
@@ -752,6 +753,7 @@ def concat_bench(args, d):
             "ebn0_db": args.concat_ebn0, "awgn_var": var, "R_overall": R_overall,
             "ber": float(cnt[1]) / (cnt[0] * user_bits) if cnt[0] else None,
             "codeword_errors": int(cnt[2]), "codewords": int(cnt[0]),
+            "decision_match": match,
             "cpu_baseline": {"value": None, "unit": "codewords/s", "cores": 0, "kind": "port",
                              "sample": "none: infeasible on the host at this size -- the reference's dense "
                                        "path (sparc_new.py:885-912, 1284-1294) holds A as a float64 "
@@ -772,6 +774,43 @@ def concat_bench(args, d):
                          "launches": {k: v[1] for k, v in ph.items()}}}
 
 
+def concat_decision_check(pipe, B, k):
+    """C5 glue + BP of the last timed decode against the CPU restatement on the
+    first k codewords: bit LLRs of the protected sections recomputed in float64
+    from the GPU's soft estimate (oracle/sparc_ref.beta_to_bit_probs and ldpc_bp's
+    clip/log, sparc_new.py:1118-1138,1167-1169), and oracle/bp_oracle.c sumprod2
+    (200 it) on the GPU's LLRs; the shipped f32 BP must take the oracle's
+    decisions on every block the oracle decodes (tests/test_c5_full_gpu.py makes
+    the same comparison at two Eb/N0)."""
+    import ctypes as ct
+    from oracle import bp as obp, sparc_ref
+    c, L, M = pipe.c, pipe.L, pipe.M
+    d_beta = ct.c_void_p()
+    _native.check(_native.lib().sg_dense_state_device(pipe.plan, ct.byref(d_beta), None))
+    _native.device_synchronize()
+    beta = np.empty((k, L * M), np.float32)
+    _native.check(_native.lib().sg_memcpy_d2h(_native.ptr(beta), d_beta, beta.nbytes, None))
+    nb = k * pipe.mults
+    llr = pipe.d_llr.download(np.empty((B * pipe.mults, c.N), np.float32))[:nb].astype(np.float64)
+    app = pipe.d_app.download(np.empty((B * pipe.mults, c.N), np.float32))[:nb]
+    err = 0.0
+    for b in range(k):
+        p = sparc_ref.beta_to_bit_probs(beta[b, pipe.L_unp * M:].astype(np.float64), L - pipe.L_unp, M, pipe.snp)
+        pc = np.clip(p, 1e-15, 1 - 1e-15)
+        ref = np.log(pc) - np.log(1 - pc)
+        bar = 1e-5 * np.maximum(1.0, np.abs(ref)) + 4e-16 / np.minimum(pc, 1 - pc)
+        err = max(err, float(np.max(np.abs(llr[b * pipe.mults:(b + 1) * pipe.mults].ravel() - ref) / bar)))
+    oapp, oit = obp.decode_batch("sumprod2", llr, c.vdeg, c.cdeg, c.intrlv, pipe.bp_its)
+    conv = oit < pipe.bp_its
+    same = ((app < 0) == (oapp < 0)).all(axis=1)
+    return {"codewords": k, "ldpc_blocks": nb, "llr_max_err_over_bar": err,
+            "blocks_oracle_decodes": int(conv.sum()),
+            "identical_block_decisions_where_oracle_decodes": float(same[conv].mean()) if conv.any() else None,
+            "identical_block_decisions": float(same.mean()),
+            "note": "LLR bar: 1e-5 x max(1, |LLR|) + the float64 conditioning of log(1 - p); oracle: "
+                    "oracle/bp_oracle.c sumprod2 in float64 on the GPU's f32 LLRs"}
+
+
 LDS_READ_B32 = 128   # B/clk/CU, ds_read_b32 (MI355X_MICROARCH.md LDS table)
 LDS_WRITE_B32 = 64   # B/clk/CU, ds_write_b32
 CLOCK_GHZ = 2.4      # max shader clock, MI355X_MICROARCH.md chip table
@@ -783,6 +822,41 @@ def bp_lds_peak_gbs(ncu):
     85.3 B/clk/CU over every CU at the maximum clock."""
     per_cu = 2.0 / (1.0 / LDS_READ_B32 + 1.0 / LDS_WRITE_B32)
     return per_cu * ncu * CLOCK_GHZ
+
+
+def summary(out):
+    """Compact per-configuration figures (value, unit, roofline fraction and its bound, decision match with the
+    CPU restatement where the run made one), repeated at the end of the line."""
+    def r(x, n=4):
+        return None if x is None else float(f"{x:.{n}g}")
+
+    def one(o, match=None):
+        if not isinstance(o, dict):
+            return None
+        rf = o.get("roofline") or {}
+        e = {"value": r(o.get("value"), 6), "frac": r(rf.get("frac")), "bound": rf.get("bound")}
+        if match is not None:
+            e["cpu_match"] = match
+        return e
+
+    def amp_match(o):
+        bm = ((o or {}).get("cpu_baseline") or {}).get("ber_match") or {}
+        return bm.get("identical_section_decisions")
+
+    s = {"C2": one(out, amp_match(out)), "C2_R1.3": one(out.get("amp_r13"), amp_match(out.get("amp_r13"))),
+         "C2_f64": one(out.get("amp_f64"), amp_match(out.get("amp_f64")))}
+    bp = out.get("bp")
+    if bp:
+        s["C3"] = one(bp, (((bp.get("cpu_baseline") or {}).get("ber_match") or {}).get("identical_codeword_decisions")))
+    for k, name in (("sc", "C4"), ("sc_notebook", "C4_notebook")):
+        if out.get(k):
+            s[name] = one(out[k], amp_match(out[k]))
+    if out.get("concat"):
+        s["C5"] = one(out["concat"], (out["concat"].get("decision_match") or {}).get(
+            "identical_block_decisions_where_oracle_decodes"))
+    rf = out.get("roofline") or {}
+    s["C2_factors"] = {"valu_issue": r(rf.get("valu_issue_frac")), "flops_per_lane": r(rf.get("flops_per_lane_instr"))}
+    return {k: v for k, v in s.items() if v is not None}
 
 
 def main():
@@ -1016,6 +1090,7 @@ def main():
         out["cpu_baseline"] = amp_cpu_baseline(st, args, args.cpu_seconds, procs)
         if not args.no_bp:
             out["bp"]["cpu_baseline"] = bp_cpu_baseline(bst, 0.4 * args.cpu_seconds, procs)
+    out["summary"] = summary(out)  # last key: inside the tail of the line a log keeps
     if d.rank == 0:
         print(json.dumps(out), flush=True)
     if comm is not None:

@@ -135,3 +135,51 @@ def test_cpu_pool_matches_serial_oracle():
     app, it, done, _ = cpu_pool.bp_decode(2, "minsum", ch, c.vdeg, c.cdeg, c.intrlv, 20, 0.7, chunk=16)
     oapp, oit = bp.decode_batch("minsum", ch, c.vdeg, c.cdeg, c.intrlv, 20, 0.7)
     assert done.all() and np.array_equal(app, oapp) and np.array_equal(it, oit)
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", BENCH)
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_summary_is_compact_and_last_key_material():
+    """The line's closing "summary" repeats every configuration's value,
+    roofline fraction and CPU decision match in a few hundred bytes (a log that
+    keeps only the line's tail still shows C3-C5)."""
+    b = _bench_module()
+    out = {"value": 10900.5, "roofline": {"frac": 0.1834, "bound": "valu-f32", "valu_issue_frac": 0.55,
+                                          "flops_per_lane_instr": 1.4},
+           "cpu_baseline": {"ber_match": {"identical_section_decisions": 0.99998}},
+           "amp_r13": {"value": 13100.0, "roofline": {}, "cpu_baseline": {"ber_match": {
+               "identical_section_decisions": 1.0}}},
+           "bp": {"value": 4.5e6, "roofline": {"frac": 0.59, "bound": "lds"},
+                  "cpu_baseline": {"ber_match": {"identical_codeword_decisions": 1.0}}},
+           "concat": {"value": 270.0, "roofline": {"frac": 0.85, "bound": "mfma"},
+                      "decision_match": {"identical_block_decisions_where_oracle_decodes": 1.0}}}
+    s = b.summary(out)
+    assert s["C2"] == {"value": 10900.5, "frac": 0.1834, "bound": "valu-f32", "cpu_match": 0.99998}
+    assert s["C3"]["cpu_match"] == 1.0 and s["C5"]["frac"] == 0.85 and s["C5"]["cpu_match"] == 1.0
+    assert s["C2_factors"] == {"valu_issue": 0.55, "flops_per_lane": 1.4}
+    assert "C4" not in s and len(json.dumps(s)) < 700
+
+
+def test_pmc_files_only_for_this_build(tmp_path, monkeypatch):
+    """bench.py reports PMC traffic / SQ figures only from a summary whose
+    lib_sha256 is the running library's."""
+    b = _bench_module()
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    monkeypatch.setattr(b, "REPO", str(tmp_path))
+    dig = b.lib_digest()
+    (prof / "r09_pmc_traffic_bench_old.json").write_text(json.dumps({"lib_sha256": "0" * 16, "amp": {
+        "kernel": "cw2_ab", "hbm_bytes_per_codeword_iteration": 1.0}}))
+    assert b.pmc_traffic("amp", "hbm_bytes_per_codeword_iteration", "cw2_") == (None, None)
+    (prof / "r09_pmc_traffic_bench_new.json").write_text(json.dumps({"lib_sha256": dig, "amp": {
+        "kernel": "cw2_ab+cw2_az", "hbm_bytes_per_codeword_iteration": 2.0}}))
+    assert b.pmc_traffic("amp", "hbm_bytes_per_codeword_iteration", "cw2_") == (2.0, "r09_pmc_traffic_bench_new.json")
+    (prof / "r09_pmc_sq_bench.json").write_text(json.dumps({"lib_sha256": dig, "amp": {
+        "valu_wave_insts_per_codeword_iteration": 5.0}}))
+    assert b.pmc_sq("amp")[0]["valu_wave_insts_per_codeword_iteration"] == 5.0
