@@ -214,6 +214,7 @@ struct Cw2Tables {
     const uint32_t *ka;       // [OT][512] a | CW_VALID | CW_NEWROW (first of its pair) | CW_ENDROW | CW_SELF
     const int32_t *oi;        // [OT][512] output index (invalid slots: 0)
     const float4 *cf;         // [OT][512] (c1, c2): output = Re(c1 H[a] + c2 conj H[N2 - a])
+    const float4 *gf;         // [OT][512] (al, be): G[a] += al z/phi, G[N2 - a] += be z/phi
     const int32_t *cls_ptr;   // [Q+1]
     const uint32_t *cls_ls;   // [Mc] padded real LDS index | section << 16
     const uint32_t *cls2;     // [Q][9216] cls_ls of each class padded to 9216 entries with CW2_TRASH
@@ -221,9 +222,8 @@ struct Cw2Tables {
     const uint16_t *seg;      // [Q][Lblk+1]
     float *xr;                // [B][2][OT][512] each half's part of Re(c1 H[a] + c2 conj H[b]) per output
     const uint2 *rab;         // [OT][512] LDS byte addresses of rows r, P - r of the slot's output (cw2_ab reads)
-    const uint4 *rec;         // [OT][2][512] Az rows record: {ka, LDS byte addresses of the slot's row writes
-                              // (rows r, P - r on the pair's last slot, else the trash slot; r = 0, P / 2: row r
-                              // and trash), 0}, then (al, be): G[a] += al z/phi, G[N2 - a] += be z/phi
+    const uint2 *wab;         // [OT][512] LDS byte addresses of the slot's row writes (rows r, P - r on the
+                              // pair's last slot, else the trash slot; r = 0, P / 2: row r and trash)
     float *vz;                // [B][OT][512] z / phi in slot order
     float *ys, *zs;           // [B][OT][512] y (copied at t = 0) and z in slot order (cw2_ctrl reads them
                               // coalesced; z in natural order is still written for a hand-over)

@@ -381,21 +381,15 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
         if (PL && m2 > h * Qh) acc_tables(tl, ka);
         float v[C2_SN];
         uint32_t e[C2_SN];
-        // the class slice; past the class's end s reads 0 and the padded table points at the trash slot
-        // (sparc.py:429-432 below writes there harmlessly).  At most 12 outputs per thread every load is
-        // in one round trip; above, one chunk at a time (all 18 in flight beside H spill)
-        const __amdgpu_buffer_rsrc_t rs0 = c2_rsrc(s + q0, 4 * (q1 - q0));
-        const __amdgpu_buffer_rsrc_t re = c2_rsrc(tb.cls2 + (size_t)m2 * CW2_SLICE, 4 * CW2_SLICE);
-        auto load_chunk = [&](int c) {
+        {  // every load of the class slice in one round trip; past the class's end s reads 0 and the
+           // padded table points at the trash slot (sparc.py:429-432 below writes there harmlessly)
+            const __amdgpu_buffer_rsrc_t rs0 = c2_rsrc(s + q0, 4 * (q1 - q0));
+            const __amdgpu_buffer_rsrc_t re = c2_rsrc(tb.cls2 + (size_t)m2 * CW2_SLICE, 4 * CW2_SLICE);
 #pragma unroll
-            for (int i = c * C2_SC; i < (c + 1) * C2_SC; ++i) {
+            for (int i = 0; i < C2_SN; ++i) {
                 v[i] = c2_ldf(rs0, 4 * tl + 4 * i * C2_T, 0);
                 e[i] = c2_ldu(re, 4 * tl, 4 * i * C2_T);
             }
-        };
-        if constexpr (PL) {
-#pragma unroll
-            for (int c = 0; c < C2_NC; ++c) load_chunk(c);
         }
         // (requested before the scatter's stores: a later load would wait for them, vmcnt is in order)
         const uint32_t cmk = tb.cmask[m2 * C2_T + tl];
@@ -408,7 +402,6 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
 #pragma unroll
         for (int c = 0; c < C2_NC; ++c) {  // beta = eta(s), sparc.py:429-432, scattered into the image and
                                            // stored over s for cw2_az (its beta_prev; past the end: dropped)
-            if constexpr (!PL) load_chunk(c);
 #pragma unroll
             for (int i = c * C2_SC; i < (c + 1) * C2_SC; ++i) {
                 const int sec = e[i] >> 16;
@@ -589,38 +582,38 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
         };
         {  // rows r and P - r of each owned pair: sum of al v conj(W) / be v W over its outputs (v = z / phi),
            // branch-free: every slot accumulates (NEWROW restarts the sums) and writes both rows, at the
-           // addresses of the host record table -- the pair's rows on its last slot, the trash slot otherwise
+           // addresses of the host table wab -- the pair's rows on its last slot, the trash slot otherwise
            // (invalid slots: al = be = 0); the two pairs whose rows coincide (r = 0, P / 2) then write their
            // sum.  (a, al, be, v and the addresses reloaded per class from L1 / L2: held across the transform,
            // or loaded one class ahead, they spill; al v and be v precomputed per codeword were slower -- four
            // times the per-codeword bytes re-read from L2 every class.)
-            constexpr int CH = (OT + 1) / 2;  // slots per load round (two rounds: in one, 12 records spill)
-            // the slot's record {a | flags, row addresses} and (al, be): two 16-byte loads from one buffer
-            // resource (rec, [OT][2][512]), and z / phi of the codeword
-            const __amdgpu_buffer_rsrc_t rr = c2_rsrc(tb.rec, 32 * OT * C2_T), rv = c2_rsrc(vz, 4 * OT * C2_T);
+            constexpr int CH = OT > 12 ? (OT + 1) / 2 : OT;  // slots per load round (one round at 12 per thread)
+            const __amdgpu_buffer_rsrc_t rg = c2_rsrc(tb.gf, 16 * OT * C2_T), rv = c2_rsrc(vz, 4 * OT * C2_T),
+                                         rk = c2_rsrc(tb.ka, 4 * OT * C2_T), rw = c2_rsrc(tb.wab, 8 * OT * C2_T);
             cx<float> u0{0.f, 0.f}, u1{0.f, 0.f};
 #pragma unroll
             for (int j0 = 0; j0 < OT; j0 += CH) {
-                uint3 rc[CH];
+                uint32_t ka[CH];
                 float4 gc[CH];
                 float vv[CH];
+                uint2 wa[CH];
 #pragma unroll
                 for (int i = 0; i < CH; ++i) {
                     const int j = j0 + i < OT ? j0 + i : OT - 1;
-                    const auto r3 = __builtin_amdgcn_raw_buffer_load_b96(rr, 16 * tl, 32 * j * C2_T, 0);
-                    rc[i] = uint3{r3[0], r3[1], r3[2]};
-                    gc[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rr, 16 * tl, (32 * j + 16) * C2_T, 0));
+                    ka[i] = c2_ldu(rk, 4 * tl, 4 * j * C2_T);
+                    gc[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, 16 * tl, 16 * j * C2_T, 0));
                     vv[i] = c2_ldf(rv, 4 * tl, 4 * j * C2_T);
+                    wa[i] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rw, 8 * tl, 8 * j * C2_T, 0));
                 }
 #pragma unroll
                 for (int j = 0; j < CH; ++j) {
                     if (j0 + j >= OT) break;
-                    const uint32_t k = rc[j].x;
+                    const uint32_t k = ka[j];
                     const cx<float> w = c2_w(tb, __umul24((uint32_t)m2, k & CW_KMASK));  // (a < 2^19, m2 < 2^6)
                     const float keep = (k & CW_NEWROW) ? 0.f : 1.f;
                     u0 = cmacc_pk({u0.x * keep, u0.y * keep}, {gc[j].x * vv[j], gc[j].y * vv[j]}, w);
                     u1 = cmac_pk({u1.x * keep, u1.y * keep}, {gc[j].z * vv[j], gc[j].w * vv[j]}, w);
-                    c2lds *pa = (c2lds *)(size_t)rc[j].y, *pb = (c2lds *)(size_t)rc[j].z;
+                    c2lds *pa = (c2lds *)(size_t)wa[j].x, *pb = (c2lds *)(size_t)wa[j].y;
                     *pa = c2f{u0.x, u0.y};
                     *pb = c2f{u1.x, u1.y};
                     if (k & CW_SELF) *pa = c2f{u0.x + u1.x, u0.y + u1.y};

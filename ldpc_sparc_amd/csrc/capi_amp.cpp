@@ -76,8 +76,8 @@ struct sg_amp_plan {
     int cw2OT = 0;
     uint32_t *c2_ka = nullptr, *c2_cmask = nullptr, *c2_cls = nullptr;
     int32_t *c2_oi = nullptr;
-    uint32_t *c2_rab = nullptr, *c2_rec = nullptr;
-    void *c2_cf = nullptr;
+    uint32_t *c2_wab = nullptr, *c2_rab = nullptr;
+    void *c2_cf = nullptr, *c2_gf = nullptr;
     void *ws_c2xp = nullptr, *ws_c2vz = nullptr, *ws_c2part = nullptr, *ws_c2ys = nullptr, *ws_c2zs = nullptr;
     uint16_t *c_cmask = nullptr;  // [Q + 1][1024] per-codeword engine: written image values per thread
     int32_t *c_oa = nullptr, *c_ob = nullptr, *c_gi = nullptr;
@@ -614,23 +614,13 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
     SG_TRY(upload(p, &p->c2_cmask, cmask));
     SG_TRY(upload(p, &p->c2_ka, ka));
     SG_TRY(upload(p, &p->c2_oi, oi));
+    SG_TRY(upload(p, &p->c2_wab, wab));
     SG_TRY(upload(p, &p->c2_rab, rab));
-    // the Az rows' per-slot record [OT][2][T] uint4: {a | flags, row write addresses, 0}, (al, be) -- two
-    // 16-byte loads per slot from one buffer resource (amp_cw2.hip cw2_az)
-    std::vector<uint32_t> rec((size_t)OT * 2 * T * 4, 0u);
-    for (int j = 0; j < OT; ++j)
-        for (int tid = 0; tid < T; ++tid) {
-            const size_t c = (size_t)j * T + tid, lo = ((size_t)(2 * j) * T + tid) * 4,
-                         hi = ((size_t)(2 * j + 1) * T + tid) * 4;
-            rec[lo] = ka[c];
-            rec[lo + 1] = wab[2 * c];
-            rec[lo + 2] = wab[2 * c + 1];
-            std::memcpy(&rec[hi], &gf[4 * c], 16);
-        }
-    SG_TRY(upload(p, &p->c2_rec, rec));
-    float *dcf = nullptr;
+    float *dcf = nullptr, *dgf = nullptr;
     SG_TRY(upload(p, &dcf, cf));
+    SG_TRY(upload(p, &dgf, gf));
     p->c2_cf = dcf;
+    p->c2_gf = dgf;
     p->cw2OT = OT;
     return SG_OK;
 }
@@ -917,9 +907,9 @@ static Cw2Tables c2tables(const sg_amp_plan *p, int B) {
     tb.OT = p->cw2OT; tb.maxcls = p->rmaxcls;
     tb.inv_n2 = 1.0f / (float)p->N2;
     tb.cmask = p->c2_cmask; tb.ka = p->c2_ka; tb.oi = p->c2_oi;
-    tb.cf = (const float4 *)p->c2_cf;
+    tb.cf = (const float4 *)p->c2_cf; tb.gf = (const float4 *)p->c2_gf;
     tb.cls_ptr = p->r_cls_ptr; tb.cls_ls = p->r_cls_ls; tb.cls2 = p->c2_cls; tb.qpos = p->r_qpos; tb.seg = p->r_seg;
-    tb.xr = (float *)p->ws_c2xp; tb.vz = (float *)p->ws_c2vz; tb.ys = (float *)p->ws_c2ys; tb.zs = (float *)p->ws_c2zs; tb.rec = (const uint4 *)p->c2_rec; tb.rab = (const uint2 *)p->c2_rab; tb.part = (float4 *)p->ws_c2part;
+    tb.xr = (float *)p->ws_c2xp; tb.vz = (float *)p->ws_c2vz; tb.ys = (float *)p->ws_c2ys; tb.zs = (float *)p->ws_c2zs; tb.wab = (const uint2 *)p->c2_wab; tb.rab = (const uint2 *)p->c2_rab; tb.part = (float4 *)p->ws_c2part;
     // [2 B][64] stamps, only when the diagnostics buffer holds them (build_cw2
     // accepts any even Q, and B * Q * 20 < 128 B for Q < 7)
     tb.tprof = (p->tprof && p->tprof_items * 20 >= (size_t)128 * B) ? p->tprof : nullptr;
