@@ -654,10 +654,11 @@ __global__ __launch_bounds__(1024) void reg_merge(RegTables<T> tb, RegBufs<T> bf
                         }
                 }
                 T R1 = T(0), R2 = T(0);
-                for (int m0 = 0; m0 < tb.Q; m0 += MC) {
-                    T mv[MC], s1[MC], s2[MC];
+                constexpr int MC2 = MC / 2;  // three loads a partial: half the chunk (at MC, 12 VGPRs spilled)
+                for (int m0 = 0; m0 < tb.Q; m0 += MC2) {
+                    T mv[MC2], s1[MC2], s2[MC2];
 #pragma unroll
-                    for (int i = 0; i < MC; ++i) {
+                    for (int i = 0; i < MC2; ++i) {
                         const T *p = pm + (size_t)(m0 + i) * 3 * Lb;
                         const bool in = m0 + i < tb.Q;
                         mv[i] = in ? p[ll] : T(-INFINITY);
@@ -665,7 +666,7 @@ __global__ __launch_bounds__(1024) void reg_merge(RegTables<T> tb, RegBufs<T> bf
                         s2[i] = in ? p[2 * Lb + ll] : T(0);
                     }
 #pragma unroll
-                    for (int i = 0; i < MC; ++i) {
+                    for (int i = 0; i < MC2; ++i) {
                         if (!(mv[i] > -INFINITY)) continue;  // empty segment
                         if (m0 + i == pmx) {
                             R1 += s1[i];

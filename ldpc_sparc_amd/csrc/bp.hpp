@@ -37,6 +37,9 @@ constexpr int GRP_WAVES = BP_THREADS / 64;
 constexpr int GRP_MAXDV = 16;  // variable degrees the unrolled variable groups take
 constexpr int GRP_MAXDC = 8;   // check degrees the unrolled check groups take
 constexpr int GRP_FLAG_BYTES = 2 * GRP_WAVES * 4;  // LDS stop flags after the messages (the whole image)
+constexpr int GRP_PAIR = 1 << 8;  // degree-word flag: this variable group and the next one run as a pair
+constexpr int GRP_PAIR_MAXD = 3;  // variable degrees whose groups pair up (the pair's slots and messages stay
+                                  // within the <4, 2> kernel's 64 VGPRs)
 struct BpGrpArgs {
     const int32_t *meta;      // [5][GRP_WAVES][VJ or CJ]: vdeg, vtab, cdeg, caddr, cvalid (see bp.hip)
     const int32_t *vmap;      // [GRP_WAVES][VJ][64] variable of each lane (-1: dummy)

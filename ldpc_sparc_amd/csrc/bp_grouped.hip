@@ -75,6 +75,49 @@ __device__ __forceinline__ float grp_var(const uint16_t *gtab, float acc, uint32
     }
 }
 
+// Two variable groups of one degree D run together: both groups' table
+// loads, then both groups' LDS reads, are in flight at once (one chain of
+// round trips for the pair instead of two).  Each variable still sums its
+// ports in the reference's order.
+template <int D, bool F2>
+__device__ __forceinline__ void grp_var2(const uint16_t *gt0, const uint16_t *gt1, float &acc0, float &acc1,
+                                         uint32_t f0, uint32_t f1) {
+    uint32_t s0[D], s1[D];
+    float m0[D], m1[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        s0[k] = (F2 && k == 0) ? (f0 & 0xffffu) : (F2 && k == 1) ? (f0 >> 16) : (uint32_t)gt0[64 * k];
+        s1[k] = (F2 && k == 0) ? (f1 & 0xffffu) : (F2 && k == 1) ? (f1 >> 16) : (uint32_t)gt1[64 * k];
+    }
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        m0[k] = *ldsf(s0[k]);
+        m1[k] = *ldsf(s1[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        acc0 += m0[k];
+        acc1 += m1[k];
+    }
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        *ldsf(s0[k]) = acc0 - m0[k];
+        *ldsf(s1[k]) = acc1 - m1[k];
+    }
+}
+
+template <bool F2>
+__device__ __forceinline__ void grp_var2_d(int d, const uint16_t *gt0, const uint16_t *gt1, float &acc0,
+                                           float &acc1, uint32_t f0, uint32_t f1) {
+    static_assert(GRP_PAIR_MAXD == 3, "pair degrees");
+    switch (d) {
+        case 1: grp_var2<1, F2>(gt0, gt1, acc0, acc1, f0, f1); break;
+        case 2: grp_var2<2, F2>(gt0, gt1, acc0, acc1, f0, f1); break;
+        case 3: grp_var2<3, F2>(gt0, gt1, acc0, acc1, f0, f1); break;
+        default: break;  // (the host pairs degrees 1..GRP_PAIR_MAXD only)
+    }
+}
+
 template <int DC>
 __device__ __forceinline__ uint32_t grp_check(uint32_t addr, float factor, uint32_t fsign) {
     float L[DC];
@@ -145,9 +188,12 @@ __global__ __launch_bounds__(BP_THREADS, VJ <= 4 ? 8 : 6) void bp_grouped_minsum
     const int32_t *mc = a.meta + 2 * GRP_WAVES * VJ + wave * CJ;
     int vd[VJ];
     uint32_t vt[VJ];
+    bool vpair[VJ];  // groups j and j + 1 (j even) run as a pair (GRP_PAIR)
 #pragma unroll
     for (int j = 0; j < VJ; ++j) {
-        vd[j] = __builtin_amdgcn_readfirstlane(mv[j]);
+        const int w = __builtin_amdgcn_readfirstlane(mv[j]);
+        vd[j] = w & (GRP_PAIR - 1);
+        vpair[j] = (j & 1) == 0 && (w & GRP_PAIR) != 0;
         vt[j] = (uint32_t)__builtin_amdgcn_readfirstlane(mv[GRP_WAVES * VJ + j]) >> 1;  // table entry
     }
     int cdg[CJ], cn[CJ];
@@ -186,10 +232,23 @@ __global__ __launch_bounds__(BP_THREADS, VJ <= 4 ? 8 : 6) void bp_grouped_minsum
         __syncthreads();
         int it = 0;
         for (; it < a.max_it; ++it) {
-            // ---- variable pass (c_ldpc.c:171-178)
+            // ---- variable pass (c_ldpc.c:171-178): groups 2i and 2i + 1 as a pair
+            // when the host flagged one (pairs sit at even positions)
 #pragma unroll
-            for (int j = 0; j < VJ; ++j)
-                if (j < a.vj) apv[j] = grp_var_d<F2>(vd[j], a.vtab + vt[j] + lane, chv[j], first2[j]);
+            for (int j = 0; j < VJ; j += 2) {
+                if (j >= a.vj) continue;
+                if (vpair[j]) {
+                    float a0 = chv[j], a1 = chv[j + 1];
+                    grp_var2_d<F2>(vd[j], a.vtab + vt[j] + lane, a.vtab + vt[j + 1] + lane, a0, a1, first2[j],
+                                   first2[j + 1]);
+                    apv[j] = a0;
+                    apv[j + 1] = a1;
+                } else {
+                    apv[j] = grp_var_d<F2>(vd[j], a.vtab + vt[j] + lane, chv[j], first2[j]);
+                    if (j + 1 < a.vj) apv[j + 1] = grp_var_d<F2>(vd[j + 1], a.vtab + vt[j + 1] + lane, chv[j + 1],
+                                                                first2[j + 1]);
+                }
+            }
             __syncthreads();
             // ---- check pass (c_ldpc.c:183-194 with the min-sum update)
             uint32_t unsat = 0u;

@@ -50,6 +50,12 @@ static void lpt_waves(const std::vector<int> &w, int cap, std::vector<int> &wave
     }
 }
 
+// Pairs of equal-degree variable groups run together (SG_BP_PAIR=0: one group at a time; A/B knob)
+static bool grp_pairs() {
+    const char *e = std::getenv("SG_BP_PAIR");
+    return !(e && std::strcmp(e, "0") == 0);
+}
+
 // Degree-grouped layout (bp.hpp BpGrpArgs) of the graph, or false when the
 // graph does not fit the grouped kernel (degrees, group counts, 16-bit LDS
 // byte addresses).  voff/coff are the port offsets, intrlv the reference's
@@ -95,6 +101,36 @@ static bool build_groups(sg_graph *g, const int64_t *vdeg, const int64_t *cdeg, 
     std::vector<int> vweight(nvg);
     for (int i = 0; i < nvg; ++i) vweight[i] = vg_deg[i] + 1;  // + the group's fixed cost
     lpt_waves(vweight, vj, vw, vp);
+    // within each wave, groups of one pairable degree (GRP_PAIR_MAXD) side by side: the kernel runs such a
+    // pair's chains together (grp_var2), the first of the pair flagged with GRP_PAIR in its degree word
+    std::vector<char> pair_first(nvg, 0);
+    for (int w = 0; w < GRP_WAVES; ++w) {
+        std::vector<int> mine;
+        for (int i = 0; i < nvg; ++i)
+            if (vw[i] == w) mine.push_back(i);
+        std::stable_sort(mine.begin(), mine.end(), [&](int x, int y) { return vp[x] < vp[y]; });
+        // pairs first (so every pair starts at an even position), then the single groups
+        std::vector<int> ord, singles;
+        std::vector<char> used(mine.size(), 0);
+        for (size_t a = 0; a < mine.size(); ++a) {
+            if (used[a]) continue;
+            used[a] = 1;
+            size_t b = a + 1;
+            if (vg_deg[mine[a]] >= 1 && vg_deg[mine[a]] <= GRP_PAIR_MAXD)
+                for (; b < mine.size(); ++b)
+                    if (!used[b] && vg_deg[mine[b]] == vg_deg[mine[a]]) break;
+            if (b < mine.size() && vg_deg[mine[a]] >= 1 && vg_deg[mine[a]] <= GRP_PAIR_MAXD) {
+                used[b] = 1;
+                pair_first[mine[a]] = 1;
+                ord.push_back(mine[a]);
+                ord.push_back(mine[b]);
+            } else {
+                singles.push_back(mine[a]);
+            }
+        }
+        ord.insert(ord.end(), singles.begin(), singles.end());
+        for (size_t q = 0; q < ord.size(); ++q) vp[ord[q]] = (int)q;
+    }
     std::vector<int32_t> meta(2 * GRP_WAVES * KVJ + 3 * GRP_WAVES * KCJ, 0);
     int32_t *m_vdeg = meta.data(), *m_vtab = m_vdeg + GRP_WAVES * KVJ;
     int32_t *m_cdeg = m_vtab + GRP_WAVES * KVJ, *m_caddr = m_cdeg + GRP_WAVES * KCJ, *m_cval = m_caddr + GRP_WAVES * KCJ;
@@ -128,7 +164,7 @@ static bool build_groups(sg_graph *g, const int64_t *vdeg, const int64_t *cdeg, 
             for (int i = 0; i < nvg; ++i)
                 if (vw[i] == w && vp[i] == j) {
                     const int d = vg_deg[i];
-                    m_vdeg[w * KVJ + j] = d;
+                    m_vdeg[w * KVJ + j] = d | (pair_first[i] && grp_pairs() ? GRP_PAIR : 0);
                     m_vtab[w * KVJ + j] = (int32_t)(2 * vtab.size());
                     const size_t off = vtab.size();
                     vtab.resize(off + 64 * (size_t)d, (uint16_t)trash);
