@@ -166,6 +166,17 @@ int sg_ldpc_graph_info(const sg_graph *g, int *nv, int *nc, int *nmsg, int *max_
  * for the degree-grouped single-precision min-sum kernel, "bp_flood_kernel<float,
  * 1, 8, 4>" for the table kernel); NUL-terminated, truncated to len bytes. */
 int sg_ldpc_decode_kernel(const sg_graph *g, int dectype, int precision, char *name, size_t len);
+/* The degree-grouped layout the single-precision min-sum kernel would use for
+ * a graph (bp.hpp BpGrpArgs), computed on the host with no device: info[10] =
+ * {grouped (1) or table kernel (0), variable / check groups per wave, the
+ * kernel instance's groups per wave (2), message image bytes, port-table
+ * entries, variable-group pairs, meta and vmap lengths}; meta / vmap / vtab are
+ * copied out when non-null (call once with nulls for the sizes).  pairs: run
+ * equal-degree variable groups in pairs (the decode default; SG_BP_PAIR=0
+ * turns it off there).  For tests that emulate the kernel on the CPU. */
+int sg_ldpc_grouped_layout(const int64_t *vdeg, const int64_t *cdeg, const int64_t *intrlv, int nv, int nc,
+                           int nmsg, int pairs, int32_t *info, int32_t *meta, int meta_cap, int32_t *vmap,
+                           int vmap_cap, uint16_t *vtab, int vtab_cap);
 
 /* Batched flooding BP (replaces one c_ldpc.c sumprod/sumprod2/minsum call per
  * codeword, c_ldpc.c:32,138,339; driven serially by ldpc.py:463-490 and

@@ -57,6 +57,8 @@ SIGNATURES = [
     ("sg_ldpc_graph_destroy", ct.c_int, [vp]),
     ("sg_ldpc_graph_info", ct.c_int, [vp] + [ct.POINTER(ct.c_int)] * 5),
     ("sg_ldpc_decode_kernel", ct.c_int, [vp, ct.c_int, ct.c_int, ct.c_char_p, ct.c_size_t]),
+    ("sg_ldpc_grouped_layout", ct.c_int, [vp, vp, vp, ct.c_int, ct.c_int, ct.c_int, ct.c_int, vp, vp, ct.c_int, vp,
+                                          ct.c_int, vp, ct.c_int]),
     ("sg_ldpc_decode", ct.c_int, [vp, ct.c_int, ct.c_int, vp, ct.c_int, ct.c_int, ct.c_double, vp, vp]),
     ("sg_ldpc_decode_device", ct.c_int,
      [vp, ct.c_int, ct.c_int, vp, ct.c_int, ct.c_int, ct.c_double, vp, vp, vp]),

@@ -56,14 +56,22 @@ static bool grp_pairs() {
     return !(e && std::strcmp(e, "0") == 0);
 }
 
+// The degree-grouped layout of a graph (host arrays; bp.hpp BpGrpArgs)
+struct GrpLayout {
+    std::vector<int32_t> meta, vmap;
+    std::vector<uint16_t> vtab;
+    int msg_bytes = 0, vj = 0, cj = 0, npairs = 0;
+};
+
 // Degree-grouped layout (bp.hpp BpGrpArgs) of the graph, or false when the
 // graph does not fit the grouped kernel (degrees, group counts, 16-bit LDS
 // byte addresses).  voff/coff are the port offsets, intrlv the reference's
-// variable-port -> check-port map.
-static bool build_groups(sg_graph *g, const int64_t *vdeg, const int64_t *cdeg, const int64_t *intrlv,
-                         const std::vector<int32_t> &voff, const std::vector<int32_t> &coff, hipStream_t s) {
-    const int nv = g->nv, nc = g->nc;
-    if (g->max_cdeg > GRP_MAXDC || g->max_vdeg > GRP_MAXDV) return false;
+// variable-port -> check-port map.  Host only (sg_ldpc_grouped_layout exposes
+// it for CPU tests).
+static bool grp_layout(int nv, int nc, int nmsg, int max_vdeg, int max_cdeg, const int64_t *vdeg,
+                       const int64_t *cdeg, const int64_t *intrlv, const std::vector<int32_t> &voff,
+                       const std::vector<int32_t> &coff, bool pairs, GrpLayout &out) {
+    if (max_cdeg > GRP_MAXDC || max_vdeg > GRP_MAXDV) return false;
     // the per-degree check code covers degrees 2..8 only (grp_check_d): a
     // check of degree 0 or 1 takes the table kernel
     for (int c = 0; c < nc; ++c)
@@ -153,7 +161,7 @@ static bool build_groups(sg_graph *g, const int64_t *vdeg, const int64_t *cdeg, 
     std::vector<int32_t> cslot_base(nc);
     for (int i = 0; i < ncg; ++i)
         for (int l = 0; l < cg_n[i]; ++l) cslot_base[corder[cg_first[i] + l]] = caddr[i] + 4 * l;
-    std::vector<int32_t> msg_addr(g->nmsg);
+    std::vector<int32_t> msg_addr(nmsg);
     for (int c = 0; c < nc; ++c)
         for (int k = 0; k < coff[c + 1] - coff[c]; ++k) msg_addr[coff[c] + k] = cslot_base[c] + 256 * k;
     // variable groups: table blocks [degree][64] wave by wave, lanes' variables
@@ -164,7 +172,8 @@ static bool build_groups(sg_graph *g, const int64_t *vdeg, const int64_t *cdeg, 
             for (int i = 0; i < nvg; ++i)
                 if (vw[i] == w && vp[i] == j) {
                     const int d = vg_deg[i];
-                    m_vdeg[w * KVJ + j] = d | (pair_first[i] && grp_pairs() ? GRP_PAIR : 0);
+                    m_vdeg[w * KVJ + j] = d | (pair_first[i] && pairs ? GRP_PAIR : 0);
+                    out.npairs += pair_first[i] && pairs ? 1 : 0;
                     m_vtab[w * KVJ + j] = (int32_t)(2 * vtab.size());
                     const size_t off = vtab.size();
                     vtab.resize(off + 64 * (size_t)d, (uint16_t)trash);
@@ -184,7 +193,25 @@ static bool build_groups(sg_graph *g, const int64_t *vdeg, const int64_t *cdeg, 
         if (e % 4 || e >= trash || hit[e / 4]++) return false;
         ++real;
     }
-    if (real != g->nmsg) return false;
+    if (real != nmsg) return false;
+    out.meta = std::move(meta);
+    out.vmap = std::move(vmap);
+    out.vtab = std::move(vtab);
+    out.msg_bytes = (int)msg_bytes;
+    out.vj = vj;
+    out.cj = cj;
+    return true;
+}
+
+// The grouped layout of a graph uploaded for the kernel (false: the graph takes the table kernel)
+static bool build_groups(sg_graph *g, const int64_t *vdeg, const int64_t *cdeg, const int64_t *intrlv,
+                         const std::vector<int32_t> &voff, const std::vector<int32_t> &coff, hipStream_t s) {
+    GrpLayout lay;
+    if (!grp_layout(g->nv, g->nc, g->nmsg, g->max_vdeg, g->max_cdeg, vdeg, cdeg, intrlv, voff, coff, grp_pairs(),
+                    lay))
+        return false;
+    const std::vector<int32_t> &meta = lay.meta, &vmap = lay.vmap;
+    const std::vector<uint16_t> &vtab = lay.vtab;
     bool ok = hipMalloc(&g->d_grp_meta, sizeof(int32_t) * meta.size()) == hipSuccess &&
               hipMalloc(&g->d_grp_vmap, sizeof(int32_t) * vmap.size()) == hipSuccess &&
               hipMalloc(&g->d_grp_vtab, sizeof(uint16_t) * vtab.size()) == hipSuccess;
@@ -194,9 +221,9 @@ static bool build_groups(sg_graph *g, const int64_t *vdeg, const int64_t *cdeg, 
          hipStreamSynchronize(s) == hipSuccess;
     if (!ok) return false;
     g->grp_ntab = (int)vtab.size();
-    g->grp_msg_bytes = (int)msg_bytes;
-    g->grp_vj = vj;
-    g->grp_cj = cj;
+    g->grp_msg_bytes = lay.msg_bytes;
+    g->grp_vj = lay.vj;
+    g->grp_cj = lay.cj;
     g->grp_ok = true;
     return true;
 }
@@ -442,6 +469,48 @@ int sg_ldpc_graph_info(const sg_graph *g, int *nv, int *nc, int *nmsg, int *max_
     if (nmsg) *nmsg = g->nmsg;
     if (max_cdeg) *max_cdeg = g->max_cdeg;
     if (max_vdeg) *max_vdeg = g->max_vdeg;
+    return SG_OK;
+}
+
+int sg_ldpc_grouped_layout(const int64_t *vdeg, const int64_t *cdeg, const int64_t *intrlv, int nv, int nc, int nmsg,
+                           int pairs, int32_t *info, int32_t *meta, int meta_cap, int32_t *vmap, int vmap_cap,
+                           uint16_t *vtab, int vtab_cap) {
+    using namespace sg;
+    SG_CHECK_ARG(vdeg && cdeg && intrlv && info, "null argument");
+    SG_CHECK_ARG(nv > 0 && nc > 0 && nmsg > 0, "empty graph (Nv=%d Nc=%d Nmsg=%d)", nv, nc, nmsg);
+    std::vector<int32_t> voff(nv + 1, 0), coff(nc + 1, 0);
+    int max_v = 0, max_c = 0;
+    for (int v = 0; v < nv; ++v) {
+        SG_CHECK_ARG(vdeg[v] >= 0 && vdeg[v] < 256, "variable degree %lld out of range", (long long)vdeg[v]);
+        voff[v + 1] = voff[v] + (int32_t)vdeg[v];
+        max_v = std::max(max_v, (int)vdeg[v]);
+    }
+    for (int c = 0; c < nc; ++c) {
+        SG_CHECK_ARG(cdeg[c] >= 2 && cdeg[c] < 256, "check degree %lld out of range (need 2..255)", (long long)cdeg[c]);
+        coff[c + 1] = coff[c] + (int32_t)cdeg[c];
+        max_c = std::max(max_c, (int)cdeg[c]);
+    }
+    SG_CHECK_ARG(voff[nv] == nmsg && coff[nc] == nmsg, "degree sums (%d, %d) do not match Nmsg=%d", voff[nv],
+                 coff[nc], nmsg);
+    GrpLayout lay;
+    const bool ok = grp_layout(nv, nc, nmsg, max_v, max_c, vdeg, cdeg, intrlv, voff, coff, pairs != 0, lay);
+    const int32_t v[10] = {ok ? 1 : 0, lay.vj, lay.cj, ok ? grp_kvj(lay.vj, lay.cj) : 0,
+                           ok ? grp_kcj(lay.vj, lay.cj) : 0, lay.msg_bytes, (int32_t)lay.vtab.size(), lay.npairs,
+                           (int32_t)lay.meta.size(), (int32_t)lay.vmap.size()};
+    std::copy(v, v + 10, info);
+    if (!ok) return SG_OK;
+    if (meta) {
+        SG_CHECK_ARG(meta_cap >= (int)lay.meta.size(), "meta buffer too small");
+        std::copy(lay.meta.begin(), lay.meta.end(), meta);
+    }
+    if (vmap) {
+        SG_CHECK_ARG(vmap_cap >= (int)lay.vmap.size(), "vmap buffer too small");
+        std::copy(lay.vmap.begin(), lay.vmap.end(), vmap);
+    }
+    if (vtab) {
+        SG_CHECK_ARG(vtab_cap >= (int)lay.vtab.size(), "vtab buffer too small");
+        std::copy(lay.vtab.begin(), lay.vtab.end(), vtab);
+    }
     return SG_OK;
 }
 
