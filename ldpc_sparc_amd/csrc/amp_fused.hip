@@ -82,9 +82,10 @@ __device__ __forceinline__ double reg_block_sum(double v, double *red) {
 // Workgroups of the first wave with an odd linear index start `cycles` late,
 // so that half the CUs run their memory phases while the other half computes
 // (the CUs would otherwise stay in phase and alternate between saturating HBM
-// and leaving it idle).
+// and leaving it idle).  Grids of fewer than two rounds of workgroups start
+// at once (nothing to interleave with).
 __device__ __forceinline__ void reg_stagger(int cycles) {
-    if (cycles <= 0) return;
+    if (cycles <= 0 || gridDim.x * gridDim.y * gridDim.z < 512) return;
     const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
     if (lin < 256 && (lin & 1)) {
         for (int c = 0; c < cycles; c += 8128) __builtin_amdgcn_s_sleep(127);

@@ -869,8 +869,9 @@ static RegTables<T> rtables(const sg_amp_plan *p) {
     tb.nT = p->nT; tb.L = p->L; tb.M = p->M; tb.LM = p->LM; tb.n = p->n; tb.Lc = p->Lc; tb.Mc = p->Mc;
     tb.Lblk = p->Lblk; tb.N2 = p->N2; tb.P = p->rP; tb.Q = p->rQ; tb.log2P = p->rlog2P; tb.ept = p->rept; tb.maxcls = p->rmaxcls; tb.img = p->rimg;
     {
-        const char *st = std::getenv("SG_AMP_STAGGER");  // measured best at C2: 20000 (+1.4 %)
-        tb.stagger = st ? std::atoi(st) : (p->precision == SG_F32 ? 20000 : 0);
+        // measured best at C2: 20000 (f32 staged engine +1.4 %, f64 +0.9 %: profiles/r04_f64_env_sweep.txt)
+        const char *st = std::getenv("SG_AMP_STAGGER");
+        tb.stagger = st ? std::atoi(st) : 20000;
     }
     tb.nRmax = p->nRmax; tb.nKmax = p->nKmax; tb.RB = p->RB; tb.nrb = p->nrb; tb.maxKb = p->maxKb;
     tb.nR = p->r_nR; tb.row_k1 = p->r_row_k1; tb.row_k1p = p->r_row_k1p; tb.kptr = p->r_kptr; tb.kk2 = p->r_kk2; tb.krho = p->r_krho;

@@ -1,5 +1,6 @@
 """Phase timing of the stage-1 kernels (SG_AMP_TPROF=1): mean shader-clock
-cycles per phase, per workgroup, for the C2 decode at B codewords."""
+cycles per phase, per workgroup, for the C2 decode at B codewords
+(usage: amp_tprof.py [B] [f32|f64])."""
 import ctypes as ct
 import os
 import sys
@@ -11,21 +12,23 @@ sys.path.insert(0, ".")
 from ldpc_sparc_amd import _native, sparc  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+prec = _native.SG_F64 if len(sys.argv) > 2 and sys.argv[2] == "f64" else _native.SG_F32
+es = 8 if prec == _native.SG_F64 else 4
 L, M, R = 1024, 512, 1.5
 n = int(round(L * 9 / R))
 W = np.array(15.0)
 lib = _native.lib()
 o0, o1 = sparc.generate_ordering(W, n, L * M, 0)
 op = sparc.DesignOperator(W, L, M, n, o0, o1)
-plan = op.plan(_native.SG_F32)
+plan = op.plan(prec)
 d_bits = _native.DeviceBuffer(B * L * 9)
 d_true = _native.DeviceBuffer(B * L * 4)
-d_x = _native.DeviceBuffer(B * n * 4)
-d_y = _native.DeviceBuffer(B * n * 4)
+d_x = _native.DeviceBuffer(B * n * es)
+d_y = _native.DeviceBuffer(B * n * es)
 _native.check(lib.sg_rng_bits_device(1, 0, B, L * 9, d_bits.ptr, None))
 _native.check(lib.sg_bits_to_sections_device(d_bits.ptr, B, L, 9, d_true.ptr, None))
 _native.check(lib.sg_amp_encode_device(plan, d_true.ptr, B, d_x.ptr, None))
-_native.check(lib.sg_awgn_device(_native.SG_F32, 1, 0, d_x.ptr, B, n, 1.0, d_y.ptr, None))
+_native.check(lib.sg_awgn_device(prec, 1, 0, d_x.ptr, B, n, 1.0, d_y.ptr, None))
 d_map = _native.DeviceBuffer(B * L * 4)
 d_tf = _native.DeviceBuffer(B * 4)
 for rep in range(2):
