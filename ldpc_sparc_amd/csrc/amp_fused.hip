@@ -42,6 +42,20 @@ template <>
 __device__ __forceinline__ float sm_arg<float>(float v, float m, float, float inv_tau) { return (v - m) * inv_tau; }
 template <>
 __device__ __forceinline__ double sm_arg<double>(double v, double m, double tau, double) { return v / tau - m / tau; }
+// The same with the maximum's term staged once per section (sm_stage: m / tau
+// in double -- the reference's max(x) of x = s / tau, as division by tau > 0 is
+// monotonic -- and m itself in single precision): one division per entry
+// instead of two, the same values
+template <typename T>
+__device__ __forceinline__ T sm_stage(T m, T tau) {
+    if constexpr (sizeof(T) == 8) return m / tau;
+    else return m;
+}
+template <typename T>
+__device__ __forceinline__ T sm_arg_st(T v, T ms, T tau, T inv_tau) {
+    if constexpr (sizeof(T) == 8) return v / tau - ms;
+    else return (v - ms) * inv_tau;
+}
 
 // Section statistics of the single-precision engine are kept as sums over
 // every entry but the maximum (whose term is exactly 1), so 1 - sum beta^2
@@ -126,13 +140,13 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_ab_stage1(RegT
     T tau = T(1), inv_tau = T(1);
     if (bf.mode == 0) {
         const size_t lb = (size_t)cw * tb.L + (size_t)t * tb.Lblk;
-        for (int l = tid; l < tb.Lblk; l += nthr) {
-            sM[l] = bf.stM[lb + l];
-            sI[l] = bf.stI[lb + l];
-        }
         const double tv = bf.tau[(size_t)cw * tb.Lc + t];
         tau = (T)tv;
         inv_tau = (T)(1.0 / tv);
+        for (int l = tid; l < tb.Lblk; l += nthr) {
+            sM[l] = sm_stage<T>(bf.stM[lb + l], tau);
+            sI[l] = bf.stI[lb + l];
+        }
     }
     __syncthreads();
     SG_TP(bf.tprof_ab, 1);
@@ -156,7 +170,7 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_ab_stage1(RegT
             for (int i = 0; i < REG_CH; ++i)
                 if (base + i * nthr < q1) {
                     const int l = e[i] >> 16;
-                    dr[e[i] & 0xffffu] = rexp<T>(sm_arg<T>(v[i], sM[l], tau, inv_tau)) * sI[l];
+                    dr[e[i] & 0xffffu] = rexp<T>(sm_arg_st<T>(v[i], sM[l], tau, inv_tau)) * sI[l];
                 }
         }
     } else if (bf.mode != 0) {
@@ -358,13 +372,13 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_az_stage2(RegT
     const bool have_beta = bf.mode == 0 && t_iter > 0;
     if (have_beta) {  // beta of the previous iteration = softmax(s_prev) with tau_prev
         const size_t lb = (size_t)cw * tb.L + (size_t)t * tb.Lblk;
-        for (int l = tid; l < tb.Lblk; l += nthr) {
-            sM[l] = bf.stM[lb + l];
-            sI[l] = bf.stI[lb + l];
-        }
         const double tv = bf.tau_prev[(size_t)cw * tb.Lc + t];
         tp = (T)tv;
         inv_tp = (T)(1.0 / tv);
+        for (int l = tid; l < tb.Lblk; l += nthr) {
+            sM[l] = sm_stage<T>(bf.stM[lb + l], tp);
+            sI[l] = bf.stI[lb + l];
+        }
     }
     __syncthreads();
     SG_TP(bf.tprof_az, 1);
@@ -413,7 +427,7 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_az_stage2(RegT
             if (q < qe) {
                 T b = T(0);
                 const int l = e[i] >> 16;
-                if (have_beta) b = rexp<T>(sm_arg<T>(v[i], sM[l], tp, inv_tp)) * sI[l];
+                if (have_beta) b = rexp<T>(sm_arg_st<T>(v[i], sM[l], tp, inv_tp)) * sI[l];
                 snv[c + i] = b + tau * dr[e[i] & 0xffffu];
             }
         }
@@ -473,6 +487,7 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_az_stage2(RegT
             for (int i = 0; i < RC; ++i) m = fmax(m, v[i]);
         }
         T S1 = T(0), S2 = T(0);
+        const T mst = sm_stage<T>(m, tau);
         bool seen = !kRestSums<T>;  // f32: sums over the segment without its (first) maximum
         for (int c = a; c < b; c += RC) {
             T v[RC];
@@ -481,7 +496,7 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_az_stage2(RegT
 #pragma unroll
             for (int i = 0; i < RC; ++i)
                 if (c + i < b) {
-                    T e = rexp<T>(sm_arg<T>(v[i], m, tau, inv_tau));
+                    T e = rexp<T>(sm_arg_st<T>(v[i], mst, tau, inv_tau));
                     if (!seen && v[i] == m) {
                         seen = true;
                         e = T(0);
