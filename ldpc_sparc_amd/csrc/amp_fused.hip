@@ -44,8 +44,14 @@ template <>
 __device__ __forceinline__ double sm_arg<double>(double v, double m, double tau, double) { return v / tau - m / tau; }
 // The same with the maximum's term staged once per section (sm_stage: m / tau
 // in double -- the reference's max(x) of x = s / tau, as division by tau > 0 is
-// monotonic -- and m itself in single precision): one division per entry
-// instead of two, the same values
+// monotonic -- and m itself in single precision), and v / tau as Markstein's
+// division by a fixed divisor: q = v r with r = RN(1 / tau) (inv_tau), then
+// one exact-residual correction q + (v - q tau) r, which is the correctly
+// rounded quotient, i.e. v / tau bit for bit (for -0 it gives +0, which the
+// exponent that follows cannot tell apart; tools/markstein_check.c: 10^8
+// random pairs over the decoder's range, none differ).  Three FMA-class
+// instructions instead of the ~11 of the general IEEE division, and one
+// division per entry instead of two.
 template <typename T>
 __device__ __forceinline__ T sm_stage(T m, T tau) {
     if constexpr (sizeof(T) == 8) return m / tau;
@@ -53,8 +59,12 @@ __device__ __forceinline__ T sm_stage(T m, T tau) {
 }
 template <typename T>
 __device__ __forceinline__ T sm_arg_st(T v, T ms, T tau, T inv_tau) {
-    if constexpr (sizeof(T) == 8) return v / tau - ms;
-    else return (v - ms) * inv_tau;
+    if constexpr (sizeof(T) == 8) {
+        const double q = v * inv_tau;
+        return __builtin_fma(__builtin_fma(-q, tau, v), inv_tau, q) - ms;
+    } else {
+        return (v - ms) * inv_tau;
+    }
 }
 
 // Section statistics of the single-precision engine are kept as sums over
