@@ -150,10 +150,13 @@ def test_lxor_lxfb_on_device():
         assert agg0 == oagg0 and np.array_equal(out0, oout0)
 
 
-def test_device_api_and_error_counter():
+@pytest.mark.parametrize("B", [300, 5000])
+def test_device_api_and_error_counter(B):
+    """Device decode + error counters; B = 5000 is more codewords than the
+    counter's 1024 wavefronts, so each loops over several."""
     c = code("802.11n", "1/2", 81)
     rng = np.random.default_rng(4)
-    X, ch = _awgn_batch(c, 1.25, 300, rng)
+    X, ch = _awgn_batch(c, 1.25, B, rng)
     L = _native.lib()
     g = c._device_graph()
     d_ch = _native.DeviceBuffer.from_array(ch.astype(np.float32))
@@ -175,6 +178,10 @@ def test_device_api_and_error_counter():
     assert cnt[1] == np.any(err, axis=1).sum()
     assert cnt[2] == err[:, :c.K].sum()
     assert cnt[3] == it.sum()
+    d_be = _native.DeviceBuffer(B * 4)
+    _native.check(L.sg_ldpc_codeword_errors_device(g, _native.SG_F32, d_app.ptr, d_x.ptr, B, d_be.ptr, None))
+    _native.synchronize()
+    assert np.array_equal(d_be.download(np.zeros(B, np.int32)), err.sum(axis=1))
 
 
 @pytest.mark.parametrize("std,rate,z", [("802.11n", "5/6", 81), ("802.16", "5/6", 96), ("802.11n", "3/4", 54)])
