@@ -478,37 +478,42 @@ __global__ __launch_bounds__(C2_T) void cw2_ctrl(Cw2Tables tb, RegBufs<float> bf
     float zr[OT];
     double acc = 0.0;
     {
+        // every load first, in one round trip (the uniform branch outside the slot loops: written per slot,
+        // with the stores between, the compiler waited for each slot's loads in turn -- 36 dependent round
+        // trips per launch); invalid slots: output 0, unused
         int oi[OT];
-        float yv[OT], zv[OT];
+        uint32_t kv[OT];
+        float yv[OT], zv[OT], r0[OT], r1[OT];
         float *ys = tb.ys + (size_t)cw * OT * C2_T, *zs = tb.zs + (size_t)cw * OT * C2_T;
 #pragma unroll
-        for (int j = 0; j < OT; ++j) {  // every load issued together (invalid slots: output 0, unused)
+        for (int j = 0; j < OT; ++j) {
             oi[j] = tb.oi[j * C2_T + tid];
-            if (have_beta) {  // y and the previous z in slot order: one coalesced round trip
+            kv[j] = tb.ka[j * C2_T + tid];
+        }
+        if (have_beta) {  // y, the previous z and the two halves' parts in slot order: coalesced
+#pragma unroll
+            for (int j = 0; j < OT; ++j) {
                 yv[j] = ys[j * C2_T + tid];
                 zv[j] = zs[j * C2_T + tid];
-            } else {  // first iteration: gather y and keep it in slot order
-                yv[j] = y[oi[j]];
-                zv[j] = 0.f;
+                r0[j] = xr0[j * C2_T + tid];
+                r1[j] = xr1[j * C2_T + tid];
             }
-        }
-        if (!have_beta) {
 #pragma unroll
-            for (int j = 0; j < OT; ++j) ys[j * C2_T + tid] = yv[j];
-        }
+            for (int j = 0; j < OT; ++j)  // Onsager residual, sparc.py:943-946; r = Re(c1 H[a] + c2 conj H[b])
+                zr[j] = (yv[j] - (r0[j] + r1[j])) + bco * zv[j];
+        } else {  // first iteration: gather y and keep it in slot order
 #pragma unroll
-        for (int j = 0; j < OT; ++j) {
-            float zn = yv[j];
-            if (have_beta) {  // Onsager residual, sparc.py:943-946
-                const float r = xr0[j * C2_T + tid] + xr1[j * C2_T + tid];  // Re(c1 H[a] + c2 conj H[b])
-                zn = (yv[j] - r) + bco * zv[j];
+            for (int j = 0; j < OT; ++j) yv[j] = y[oi[j]];
+#pragma unroll
+            for (int j = 0; j < OT; ++j) {
+                ys[j * C2_T + tid] = yv[j];
+                zr[j] = yv[j];
             }
-            zr[j] = zn;
         }
 #pragma unroll
         for (int j = 0; j < OT; ++j) {
             zs[j * C2_T + tid] = zr[j];
-            if (tb.ka[j * C2_T + tid] & CW_VALID) {
+            if (kv[j] & CW_VALID) {
                 z[oi[j]] = zr[j];  // (natural order: the staged engine's after a hand-over)
                 if (sum_z) acc += (double)zr[j] * (double)zr[j];
             }
@@ -758,8 +763,10 @@ __global__ __launch_bounds__(1024) void cw2_merge(Cw2Tables tb, RegBufs<float> b
     if (tid < Lb) {
         const float4 *part = tb.part + (size_t)cw * 2 * Lb;
         float Mr = -INFINITY, R1 = 0.f, R2 = 0.f, s_true = NAN;
+        const float4 ph[2] = {part[tid], part[Lb + tid]};  // (both requested together)
+#pragma unroll
         for (int h = 0; h < 2; ++h) {  // the halves in order: same merge as the class merge of cw2_az
-            const float4 p = part[h * Lb + tid];
+            const float4 p = ph[h];
             const float m = p.x;
             if (!(p.w != p.w)) s_true = p.w;
             if (m > -INFINITY) {
