@@ -301,13 +301,50 @@ __global__ __launch_bounds__(1024) void control_kernel(AmpTables<T> tb, AmpBufs<
             }
             __syncthreads();
             for (int c = tid; c < Lc; c += blockDim.x) psi_prev[c] = psi[c];
-            // z = y - Ab(beta) + b*z, Ab summed over the transforms of each row block
-            for (int i = tid; i < tb.n; i += blockDim.x) {
-                const int r = i / tb.Mr, il = i - r * tb.Mr;
-                T ab = T(0);
-                for (int q = tb.row_ptr[r]; q < tb.row_ptr[r + 1]; ++q)
-                    ab += bf.rbuf[((size_t)cw * tb.nT + tb.row_t[q]) * tb.Mr + il];
-                z[i] = (y[i] - ab) + (T)bco[r] * z[i];
+            // z = y - Ab(beta) + b*z, Ab summed over the transforms of each row block in table order.
+            // ZU entries per thread at a time with the first QM transforms of each row requested
+            // together, unconditionally (indices clamped into the tables, values masked): as a plain loop
+            // every entry's table -> transform index -> rbuf chain, and each transform's load, was its
+            // own round trip
+            constexpr int ZU = 2, QM = 8;  // (ZU = 4 spilled at the 1024-thread kernel's 128 VGPRs)
+            const int qlast = tb.row_ptr[Lr] - 1;
+            for (int b0 = tid; b0 < tb.n; b0 += ZU * (int)blockDim.x) {
+                int rr[ZU], qa[ZU], qb[ZU], il[ZU];
+                T yv[ZU], zv[ZU];
+                double bv[ZU];
+#pragma unroll
+                for (int u = 0; u < ZU; ++u) {
+                    const int i = min(b0 + u * (int)blockDim.x, tb.n - 1);
+                    const int r = i / tb.Mr;
+                    rr[u] = r;
+                    il[u] = i - r * tb.Mr;
+                    qa[u] = tb.row_ptr[r];
+                    qb[u] = tb.row_ptr[r + 1];
+                    yv[u] = y[i];
+                    zv[u] = z[i];
+                    bv[u] = bco[r];
+                }
+                T rv[ZU][QM];
+#pragma unroll
+                for (int u = 0; u < ZU; ++u) {
+                    int tq[QM];
+#pragma unroll
+                    for (int k = 0; k < QM; ++k) tq[k] = tb.row_t[min(qa[u] + k, qlast)];
+#pragma unroll
+                    for (int k = 0; k < QM; ++k) rv[u][k] = bf.rbuf[((size_t)cw * tb.nT + tq[k]) * tb.Mr + il[u]];
+                }
+#pragma unroll
+                for (int u = 0; u < ZU; ++u) {
+                    const int i = b0 + u * (int)blockDim.x;
+                    if (i >= tb.n) continue;
+                    T ab = T(0);
+#pragma unroll
+                    for (int k = 0; k < QM; ++k)
+                        if (qa[u] + k < qb[u]) ab += rv[u][k];
+                    for (int q = qa[u] + QM; q < qb[u]; ++q)  // (rows of more than QM transforms)
+                        ab += bf.rbuf[((size_t)cw * tb.nT + tb.row_t[q]) * tb.Mr + il[u]];
+                    z[i] = (yv[u] - ab) + (T)bv[u] * zv[u];
+                }
             }
         } else {
             for (int i = tid; i < tb.n; i += blockDim.x) z[i] = y[i];
