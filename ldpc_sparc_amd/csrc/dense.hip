@@ -254,6 +254,7 @@ __device__ __forceinline__ float dexp2<float>(float x) { return __expf(x); }
 template <>
 __device__ __forceinline__ double dexp2<double>(double x) { return exp(x); }
 
+constexpr int DETA_R = 16;  // entries per lane held in registers (sections of M <= 1024)
 template <typename T>
 __global__ __launch_bounds__(256) void dense_eta_kernel(DenseBufs<T> d) {
     const int lane = threadIdx.x & 63;
@@ -265,16 +266,47 @@ __global__ __launch_bounds__(256) void dense_eta_kernel(DenseBufs<T> d) {
     const T *s = d.s + (long)b * d.LM + (long)l * d.M;
     T *beta = d.beta + (long)b * d.LM + (long)l * d.M;
     T mx = -INFINITY;
-    for (int j = lane; j < d.M; j += 64) mx = fmax(mx, c * (s[j] / tau2));
-    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
-    T den = T(0);
-    for (int j = lane; j < d.M; j += 64) den += dexp2<T>(c * (s[j] / tau2) - mx);
-    for (int o = 32; o > 0; o >>= 1) den += __shfl_xor(den, o, 64);
     double sq = 0.0;
-    for (int j = lane; j < d.M; j += 64) {
-        const T v = c * (dexp2<T>(c * (s[j] / tau2) - mx) / den);
-        beta[j] = v;
-        sq += (double)v * (double)v;
+    if (d.M <= 64 * DETA_R) {
+        // the section in registers: s read once, its exponent argument and exponential computed
+        // once per entry (the loop form below re-reads s and recomputes both in every pass);
+        // the same per-entry values and per-lane summation order
+        T x[DETA_R];
+#pragma unroll
+        for (int r = 0; r < DETA_R; ++r) {
+            const int j = lane + 64 * r;
+            x[r] = j < d.M ? c * (s[j] / tau2) : T(-INFINITY);
+        }
+#pragma unroll
+        for (int r = 0; r < DETA_R; ++r) mx = fmax(mx, x[r]);
+        for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+        T den = T(0);
+#pragma unroll
+        for (int r = 0; r < DETA_R; ++r) {
+            x[r] = lane + 64 * r < d.M ? dexp2<T>(x[r] - mx) : T(0);
+            den += x[r];
+        }
+        for (int o = 32; o > 0; o >>= 1) den += __shfl_xor(den, o, 64);
+#pragma unroll
+        for (int r = 0; r < DETA_R; ++r) {
+            const int j = lane + 64 * r;
+            if (j < d.M) {
+                const T v = c * (x[r] / den);
+                beta[j] = v;
+                sq += (double)v * (double)v;
+            }
+        }
+    } else {
+        for (int j = lane; j < d.M; j += 64) mx = fmax(mx, c * (s[j] / tau2));
+        for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+        T den = T(0);
+        for (int j = lane; j < d.M; j += 64) den += dexp2<T>(c * (s[j] / tau2) - mx);
+        for (int o = 32; o > 0; o >>= 1) den += __shfl_xor(den, o, 64);
+        for (int j = lane; j < d.M; j += 64) {
+            const T v = c * (dexp2<T>(c * (s[j] / tau2) - mx) / den);
+            beta[j] = v;
+            sq += (double)v * (double)v;
+        }
     }
     for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
     if (lane == 0) d.sec_bsq[(long)b * d.L + l] = sq;
