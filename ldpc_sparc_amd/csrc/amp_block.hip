@@ -182,19 +182,30 @@ __device__ __forceinline__ void bk_ab_column(const BlkTables &tb, const AmpBufs<
 // Makhoul packing): G[k] = sum of <= 4 terms c * z_i / phi_r, one thread per
 // slot, written to gbuf so that blk_az loads each transform's slots in one
 // coalesced round trip.
+// (two dependent rounds of loads: the slot's table entries, then phi and the four z values,
+// unconditionally at clamped indices -- with a branch per term each term's z load waited on its own)
 __device__ __forceinline__ cx<float> bk_gslot(const BlkTables &tb, const AmpBufs<float> &bf, int cw, int g) {
     const int row = tb.grow[g];
+    int gi[4];
+    cx<float> gc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        gi[k] = tb.gi[4 * g + k];
+        gc[k] = tb.gc[4 * g + k];
+    }
     const float *z = bf.z + (size_t)cw * tb.n + (size_t)row * tb.Mr;
-    const float iphi = 1.0f / (float)bf.phi[(size_t)cw * tb.Lr + row];
+    const float ph = (float)bf.phi[(size_t)cw * tb.Lr + row];
+    float zv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) zv[k] = z[max(gi[k], 0)];
+    const float iphi = 1.0f / ph;
     cx<float> acc{0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const int i = tb.gi[4 * g + k];
-        if (i >= 0) {
-            const float v = z[i] * iphi;  // Az(z / phi), sparc.py:972 (one division per slot)
-            const cx<float> cc = tb.gc[4 * g + k];
-            acc.x += cc.x * v;
-            acc.y += cc.y * v;
+        if (gi[k] >= 0) {
+            const float v = zv[k] * iphi;  // Az(z / phi), sparc.py:972 (one division per slot)
+            acc.x += gc[k].x * v;
+            acc.y += gc[k].y * v;
         }
     }
     return acc;
