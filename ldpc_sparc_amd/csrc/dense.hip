@@ -126,19 +126,33 @@ __global__ __launch_bounds__(256, MT == 4 ? 2 : 1) void gemm_f32_mfma(GemmF32 g)
         }
     }
     float *C = g.C + (long)blockIdx.z * g.c_split;
+    // per 32 x 32 tile: the 16 addends requested together (clamped into the matrix, no branch), then the
+    // 16 stores -- with the load inside each output's bounds branch, every output waited for its own
+    // addend: 128 dependent round trips per thread at the end of each block
+    const int rmax = g.M - 1, cmax = g.N - 1;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
+        for (int nt = 0; nt < 2; ++nt) {
+            float av[16];
+            if (g.add) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = m0 + wm * 32 * MT + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    const int col = n0 + wn * 64 + nt * 32 + (lane & 31);
+                    av[r] = g.add[(long)min(row, rmax) * g.ldc + min(col, cmax)];
+                }
+            }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int row = m0 + wm * 32 * MT + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
                 const int col = n0 + wn * 64 + nt * 32 + (lane & 31);
                 if (row < g.M && col < g.N) {
                     const long o = (long)row * g.ldc + col;
-                    C[o] = g.add ? g.add[o] + acc[mt][nt][r] : acc[mt][nt][r];
+                    C[o] = g.add ? av[r] + acc[mt][nt][r] : acc[mt][nt][r];
                 }
             }
+        }
 }
 
 // Block rows of 256 once the batch exceeds 128 codewords (A read ceil(B / 256)
