@@ -239,10 +239,8 @@ __global__ __launch_bounds__(256) void reg_ab_stage2(RegTables<T> tb, RegBufs<T>
         for (int m0 = tid / tb.RB; m0 < tb.Q; m0 += REG_CH * mstep) {
             cx<T> v[REG_CH];
 #pragma unroll
-            for (int i = 0; i < REG_CH; ++i) {
-                const int m2 = m0 + i * mstep;
-                if (m2 < tb.Q) v[i] = sp[(size_t)m2 * tb.nRmax];
-            }
+            for (int i = 0; i < REG_CH; ++i)  // (clamped, unconditional: all REG_CH in one round trip)
+                v[i] = sp[(size_t)min(m0 + i * mstep, tb.Q - 1) * tb.nRmax];
 #pragma unroll
             for (int i = 0; i < REG_CH; ++i) {
                 const int m2 = m0 + i * mstep;
@@ -313,19 +311,30 @@ __global__ __launch_bounds__(256) void reg_az_stage1(RegTables<T> tb, RegBufs<T>
     const int32_t *gi = tb.gi + (size_t)t * tb.nKmax * 4;
     const cx<T> *gc = tb.gc + (size_t)t * tb.nKmax * 4;
     for (int k = ka + tid; k < kb; k += nthr) {
+        // the four terms' table entries, then their z values (clamped index, no branch): two
+        // rounds of loads instead of a wait per term
+        int ii[4];
+        cx<T> cc[4];
+        T zv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            ii[q] = gi[4 * k + q];
+            cc[q] = gc[4 * k + q];
+        }
+        const int k2v = tb.kk2[(size_t)t * tb.nKmax + k];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) zv[q] = z[max(ii[q], 0)];
         cx<T> acc{T(0), T(0)};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const int i = gi[4 * k + q];
-            if (i >= 0) {
-                const T v = z[i] / phi;  // Az(z / phi), sparc.py:972
-                const cx<T> c = gc[4 * k + q];
-                acc.x += c.x * v;
-                acc.y += c.y * v;
+            if (ii[q] >= 0) {
+                const T v = zv[q] / phi;  // Az(z / phi), sparc.py:972
+                acc.x += cc[q].x * v;
+                acc.y += cc[q].y * v;
             }
         }
         g[k - ka] = acc;
-        rk2[k - ka] = tb.kk2[(size_t)t * tb.nKmax + k];
+        rk2[k - ka] = k2v;
     }
     for (int r = tid; r <= nr; r += nthr) {
         rkp[r] = kp[r0 + r] - ka;
