@@ -66,6 +66,37 @@ VALU_F64_PEAK_SOURCE = ("157.3 TF f32 vector peak (MI355X_MICROARCH.md) / 2: v_f
 AMP_PHASES = ("ab_passA", "ab_passB", "az_passA", "az_passB", "eta", "control", "amp_iter")
 
 
+# Restatement-to-reference speed on one host (tools/cpu_calibrate.py, run in the
+# build container where the reference exists: the imported sparc_public/sparc.py
+# and oracle/_ref's compile of c_ldpc.c against oracle/ on the same inputs, one
+# thread each).  Quoted in every cpu_baseline so the "port" figure can be read
+# as the reference's speed.
+CALIB_FILE = os.path.join(REPO, "profiles", "r05_cpu_calibration.json")
+
+
+def calib(key):
+    try:
+        with open(CALIB_FILE) as f:
+            c = json.load(f)
+    except (OSError, ValueError):
+        return {"port_over_reference_speed": None, "source": f"{os.path.relpath(CALIB_FILE, REPO)} missing"}
+    src = {"amp_r15": ("amp_r15", "port_over_reference_speed", "C2 at R=1.5"),
+           "amp_r13": ("amp_r13", "port_over_reference_speed", "C2 at R=1.3"),
+           "bp_minsum": ("bp", "minsum_corrected", "C3 min-sum, per iteration (the reference ships the c_ldpc.c:364 "
+                                                   "defect, which never stops early)"),
+           "bp_sumprod2": ("bp", "sumprod2", "C3 code, sumprod2")}[key]
+    if src[0] == "bp":
+        e = c["bp"][src[1]]
+        r = e.get("port_over_reference_speed_per_iteration", e.get("port_over_reference_speed"))
+    else:
+        e = c[src[0]]
+        r = e[src[1]]
+    return {"port_over_reference_speed": r, "measured_on": src[2], "host": c.get("host"), "threads": 1,
+            "source": os.path.relpath(CALIB_FILE, REPO) + " (tools/cpu_calibrate.py, build container: the reference "
+                      "itself against the restatement on the same inputs)",
+            "note": "reference speed on that host = port speed / this ratio"}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -465,6 +496,7 @@ def amp_cpu_baseline(st, args, seconds, procs):
             tg = int(gtf[b])
             thr += int(abs(ps[tg - 1] - ps[tg - 2]) / abs(ps[tg - 2]) <= 1.1e-6)
     return {"value": nd / el, "unit": "codewords/s", "cores": procs, "kind": "port",
+            "vs_reference": calib("amp_r13" if abs(args.rate - 1.3) < 1e-9 else "amp_r15"),
             "sample": f"{nd} of the {B} C2 codewords the GPU decoded (R={args.rate}, t_max={args.t_max}, {iters} AMP "
                       f"iterations, {el:.1f} s wall) by oracle/sparc_ref.py (numpy/scipy fftpack DCT, float128 "
                       f"softmax), one single-threaded process per core on {procs} host cores",
@@ -526,6 +558,7 @@ def bp_cpu_baseline(st, seconds, procs):
     ch_, gh = (app[done] < 0).astype(np.int64), (gapp[done] < 0).astype(np.int64)
     ce, ge = (ch_[:, :c.K] != x), (gh[:, :c.K] != x)
     return {"value": nd / el, "unit": "codewords/s", "cores": procs, "kind": "port",
+            "vs_reference": calib("bp_minsum"),
             "sample": f"{nd} of the {st['B']} C3 codewords the GPU decoded (802.11n r1/2 z=81, min-sum, 50 it, "
                       f"Eb/N0 {st.get('ebn0')} dB, {el:.1f} s wall) by oracle/bp_oracle.c, one single-threaded "
                       f"process per core on {procs} host cores",
@@ -583,6 +616,7 @@ def bp_variant(args, d, std, rate, z, dectype, prec, ebn0, B, steps, max_it=50, 
                                                   deadline_s=cpu_seconds)
         ch_ = (capp[done] < 0).astype(np.int64)
         out["cpu_baseline"] = {"value": int(done.sum()) / cel, "unit": "codewords/s", "cores": procs, "kind": "port",
+                               "vs_reference": calib("bp_sumprod2" if dectype == "sumprod2" else "bp_minsum"),
                                "sample": f"{int(done.sum())} of the {B} codewords, oracle/bp_oracle.c on {procs} cores",
                                "identical_codeword_decisions": float((ch_ == hard[done]).all(1).mean()),
                                "identical_iteration_counts": float((cit[done] == its[done]).mean()),
@@ -693,6 +727,8 @@ def sc_bench(args, d, comm, cpu_seconds, procs, L=1024, B=None, steps=None, seed
         cmap = np.stack([res[b][0] for b in done])
         ctf = np.array([res[b][1] for b in done])
         out["cpu_baseline"] = {"value": len(done) / cel, "unit": "codewords/s", "cores": procs, "kind": "port",
+                               "vs_reference": {**calib("amp_r15"), "measured_on": "C2 at R=1.5 (same restatement "
+                                                "operators and float128 softmax; not timed on this geometry)"},
                                "sample": f"{len(done)} codewords of this geometry ({int(ctf.sum())} AMP iterations, {cel:.1f} s "
                                          "wall) decoded by oracle/sparc_ref.py (scipy fftpack DCT per block, float128 "
                                          f"softmax), one single-threaded process per core on {procs} host cores",

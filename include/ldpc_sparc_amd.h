@@ -190,8 +190,9 @@ int sg_ldpc_decode(sg_graph *g, int dectype, int precision, const double *ch, in
                    double corr, double *app, int32_t *it);
 /* Device variant: d_ch/d_app are float or double per `precision`.  SG_F32
  * min-sum on a graph of the degree-grouped layout (bp_grouped.hip) expects
- * NaN-free channel LLRs and saturates them at +-1e30; the host entry point
- * above sends a batch holding a NaN to the table kernel instead. */
+ * NaN-free channel LLRs and saturates them at +-1e30 (so +-inf decodes as
+ * +-1e30); the host entry point above sends a batch holding a NaN, an
+ * infinity or a value that overflows float to the table kernel instead. */
 int sg_ldpc_decode_device(sg_graph *g, int dectype, int precision, const void *d_ch, int B,
                           int max_it, double corr, void *d_app, int32_t *d_it, void *stream);
 /* Device-side error counting against known codewords (ldpc_awgn.py:97-104):

@@ -307,7 +307,7 @@ __global__ __launch_bounds__(1024) void control_kernel(AmpTables<T> tb, AmpBufs<
             // every entry's table -> transform index -> rbuf chain, and each transform's load, was its
             // own round trip
             constexpr int ZU = 2, QM = 8;  // (ZU = 4 spilled at the 1024-thread kernel's 128 VGPRs)
-            const int qlast = tb.row_ptr[Lr] - 1;
+            const int qlast = tb.row_ptr[Lr] - 1;  // -1: a plan with no transforms, nothing to load (uniform)
             for (int b0 = tid; b0 < tb.n; b0 += ZU * (int)blockDim.x) {
                 int rr[ZU], qa[ZU], qb[ZU], il[ZU];
                 T yv[ZU], zv[ZU];
@@ -327,6 +327,11 @@ __global__ __launch_bounds__(1024) void control_kernel(AmpTables<T> tb, AmpBufs<
                 T rv[ZU][QM];
 #pragma unroll
                 for (int u = 0; u < ZU; ++u) {
+                    if (qlast < 0) {
+#pragma unroll
+                        for (int k = 0; k < QM; ++k) rv[u][k] = T(0);
+                        continue;
+                    }
                     int tq[QM];
 #pragma unroll
                     for (int k = 0; k < QM; ++k) tq[k] = tb.row_t[min(qa[u] + k, qlast)];

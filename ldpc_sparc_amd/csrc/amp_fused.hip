@@ -46,10 +46,16 @@ __device__ __forceinline__ double sm_arg<double>(double v, double m, double tau,
 // in double -- the reference's max(x) of x = s / tau, as division by tau > 0 is
 // monotonic -- and m itself in single precision), and v / tau as Markstein's
 // division by a fixed divisor: q = v r with r = RN(1 / tau) (inv_tau), then
-// one exact-residual correction q + (v - q tau) r, which is the correctly
-// rounded quotient, i.e. v / tau bit for bit (for -0 it gives +0, which the
-// exponent that follows cannot tell apart; tools/markstein_check.c: 10^8
-// random pairs over the decoder's range, none differ).  Three FMA-class
+// one exact-residual correction q + (v - q tau) r.  Markstein's theorem makes
+// that the correctly rounded quotient when q is within one ulp of v / tau,
+// which q = RN(v r) does not guarantee in every corner, so the claim is
+// empirical: tools/markstein_check.c compares it with v / tau on 10^8 random
+// pairs of the decoder's range, 1.2e8 corner pairs (divisor significands near
+// 1 and 2, quotients just below and above powers of two) and every value of
+// the divisor's low 16 significand bits at top-of-binade quotients, and none
+// differ (for -0 it gives +0, which the exponent that follows cannot tell
+// apart; a last-ulp difference elsewhere would move one exponent argument by
+// one ulp, inside the f64 bars of DESIGN.md "Oracle and parity").  Three FMA-class
 // instructions instead of the ~11 of the general IEEE division, and one
 // division per entry instead of two.
 template <typename T>

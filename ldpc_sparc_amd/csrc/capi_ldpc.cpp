@@ -373,12 +373,14 @@ static int decode_host(sg_graph *g, int dectype, int precision, const double *ch
         SG_HIP(hipMemcpyAsync(g->d_ch, ch, n * sizeof(double), hipMemcpyHostToDevice, s));
     } else {
         std::vector<float> tmp(n);
-        bool nan = false;
+        bool nonfinite = false;
         for (size_t i = 0; i < n; ++i) {
             tmp[i] = (float)ch[i];
-            nan |= std::isnan(ch[i]);
+            nonfinite |= !std::isfinite(tmp[i]);
         }
-        ch_has_nan = nan;  // a NaN input goes to the table kernel (NaN semantics)
+        // a NaN or infinite input (or one that overflows float) goes to the table kernel: NaN and
+        // inf semantics of the reference; the grouped kernel saturates channel LLRs at +-1e30
+        ch_has_nan = nonfinite;
         SG_HIP(hipMemcpyAsync(g->d_ch, tmp.data(), n * sizeof(float), hipMemcpyHostToDevice, s));
         SG_HIP(hipStreamSynchronize(s));
     }
@@ -492,6 +494,14 @@ int sg_ldpc_grouped_layout(const int64_t *vdeg, const int64_t *cdeg, const int64
     }
     SG_CHECK_ARG(voff[nv] == nmsg && coff[nc] == nmsg, "degree sums (%d, %d) do not match Nmsg=%d", voff[nv],
                  coff[nc], nmsg);
+    {  // the same permutation check as graph creation: grp_layout indexes msg_addr[intrlv[p]]
+        std::vector<uint8_t> seen(nmsg, 0);
+        for (int p = 0; p < nmsg; ++p) {
+            const int64_t m = intrlv[p];
+            SG_CHECK_ARG(m >= 0 && m < nmsg && !seen[m], "intrlv is not a permutation of [0, Nmsg)");
+            seen[m] = 1;
+        }
+    }
     GrpLayout lay;
     const bool ok = grp_layout(nv, nc, nmsg, max_v, max_c, vdeg, cdeg, intrlv, voff, coff, pairs != 0, lay);
     const int32_t v[10] = {ok ? 1 : 0, lay.vj, lay.cj, ok ? grp_kvj(lay.vj, lay.cj) : 0,

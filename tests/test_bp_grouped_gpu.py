@@ -129,13 +129,16 @@ def test_graphs_outside_the_grouped_layout_take_the_table_kernel():
         _graph(vdeg, cdeg, intrlv)
 
 
-def test_nan_channel_input_takes_the_table_kernel(monkeypatch):
-    """The grouped kernel has no NaN semantics (built -fno-honor-nans): a host
-    batch holding a NaN decodes through the table kernel, so its results equal
-    the table kernel's."""
+@pytest.mark.parametrize("bad", [np.nan, np.inf, -np.inf, 1e300])
+def test_nonfinite_channel_input_takes_the_table_kernel(monkeypatch, bad):
+    """The grouped kernel has no NaN semantics (built -fno-honor-nans) and
+    saturates channel LLRs at +-1e30: a host batch holding a NaN, an infinity
+    (a hard-known bit) or a double that overflows float decodes through the
+    table kernel, so its results equal the table kernel's."""
     c = code("802.11n", "1/2", 27)
     ch = _awgn(c, 1.5, 8, np.random.default_rng(4))
-    ch[3, 17] = np.nan
+    ch[3, 17] = bad
+    ch[5, 3] = -bad if not np.isnan(bad) else bad
     vdeg, cdeg, intrlv = (np.asarray(a, np.int64) for a in (c.vdeg, c.cdeg, c.intrlv))
     g = _graph(vdeg, cdeg, intrlv)
     try:

@@ -175,3 +175,14 @@ def test_graphs_outside_the_layout():
     assert layout(vdeg, cdeg, intrlv) is None
     vdeg, cdeg, intrlv = _random_graph((2, 3), 200, rng, 12)  # check degrees up to 12
     assert layout(vdeg, cdeg, intrlv) is None
+
+
+@pytest.mark.parametrize("bad", ["negative", "too_large", "repeated"])
+def test_layout_refuses_a_bad_interleaver(bad):
+    """sg_ldpc_grouped_layout runs graph creation's permutation check on intrlv
+    before building the layout (which indexes msg_addr[intrlv[p]])."""
+    c = code("802.11n", "1/2", 27)
+    intrlv = np.array(c.intrlv, np.int64)
+    intrlv[5] = {"negative": -1, "too_large": len(intrlv), "repeated": intrlv[6]}[bad]
+    with pytest.raises(_native.NativeError, match="permutation"):
+        layout(c.vdeg, c.cdeg, intrlv)

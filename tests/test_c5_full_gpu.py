@@ -68,6 +68,7 @@ def _a_blocks(pipe):
 
 
 def _state(pipe, B):
+    """(beta, s) of the first B codewords of the plan's state, as float64."""
     d_beta, d_s = ct.c_void_p(), ct.c_void_p()
     _native.check(_native.lib().sg_dense_state_device(pipe.plan, ct.byref(d_beta), ct.byref(d_s)))
     _native.synchronize()
@@ -79,9 +80,9 @@ def _state(pipe, B):
     return out
 
 
-def _amp(pipe, B, t_max):
+def _amp(pipe, B, t_max, rows=None):
     _native.check(_native.lib().sg_dense_amp_device(pipe.plan, pipe.d_y.ptr, B, t_max, None, None, None))
-    return _state(pipe, B)
+    return _state(pipe, B if rows is None else rows)
 
 
 @pytest.mark.parametrize("ebn0", [4.5, 6.0])
@@ -91,6 +92,37 @@ def test_c5_one_amp_iteration_vs_float64(pipe, ebn0):
     y = pipe.d_y.download(np.empty((B, N_CH), np.float32)).astype(np.float64)
     beta1, s1 = _amp(pipe, B, 1)
     beta2, s2 = _amp(pipe, B, 2)
+    _check_vs_float64(pipe, y, beta1, s1, beta2, s2)
+
+
+def test_c5_shipped_wide_tile_b256(pipe):
+    """The instance the C5 line times: at B = 256 both GEMMs run
+    gemm_f32_mfma<*, 4> (256-row block tiles, dense.hip:160-166), at B <= 128
+    the <*, 2> form.  The batch draw of codeword b depends only on (seed,
+    stream, b), so codewords 0-7 of a 256-codeword batch are the received
+    words of an 8-codeword batch: y (x = A beta0 through the NT GEMM), beta and
+    s after one and two iterations must be bit-identical between the two
+    instances (dense.hip:24: same k-order per output), and the B = 256 rows are
+    checked against float64 products as in the test above
+    (sparc_new.py:901-910)."""
+    K = 8
+    var = _awgn_var(6.0, pipe.c)
+    got = {}
+    for B in (256, K):
+        pipe.make_batch_device(B, var, 5150, 3)
+        y = pipe.d_y.download(np.empty((B, N_CH), np.float32))[:K]
+        beta1, s1 = _amp(pipe, B, 1, rows=K)
+        beta2, s2 = _amp(pipe, B, 2, rows=K)
+        got[B] = (y, beta1, s1, beta2, s2)
+    for name, a, b in zip(("y", "beta1", "s1", "beta2", "s2"), got[256], got[K]):
+        assert np.array_equal(a, b), f"{name}: B = 256 (<*, 4>) differs from B = 8 (<*, 2>)"
+    print("  B = 256 rows 0-7 bit-identical to the B = 8 batch (y, beta, s at t = 1, 2)", flush=True)
+    y, beta1, s1, beta2, s2 = got[256]
+    _check_vs_float64(pipe, y.astype(np.float64), beta1, s1, beta2, s2)
+
+
+def _check_vs_float64(pipe, y, beta1, s1, beta2, s2):
+    B = y.shape[0]
     Pl = P / L
     snp = np.sqrt(N_CH * Pl)
     # pass 1: s1 = A^T y (beta = 0 at t = 0) and A beta1
