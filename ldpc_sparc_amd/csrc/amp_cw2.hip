@@ -45,6 +45,38 @@ constexpr int C2_SC = 9;   // class entries per thread and chunk
 constexpr int C2_NC = 2;   // chunks: a class holds at most C2_SC * C2_NC * 512 = 9216 entries
 static_assert(C2_EPT == 16, "the transform is written for 16 values per thread");
 
+// Phase ablation for timing studies only (tools/c2_ablate.py on variants built by
+// tools/mk_variant.sh with -DC2_ABL=<mask>; results are garbage, the shipped build has 0):
+// 1 Ab FFT, 2 Ab accumulation, 4 Ab slice loads, 8 Az FFT, 16 Az rows, 32 Az rows' table
+// loads (values from the thread index), 64 Az statistics + class copy, 128 Az slice loads
+#ifndef C2_ABL
+#define C2_ABL 0
+#endif
+#define C2_SKIP(bit) ((C2_ABL & (bit)) != 0)
+
+// Start stagger (A/B: -DC2_STAGGER=<cycles> -DC2_STAGGER_SEL=<rule>): two workgroups share a CU and run
+// the same class loop; started together they stay in phase (both load, then both transform).  The
+// selected workgroups of the first wave sleep `cycles` at entry, about half a class, so one
+// workgroup's memory phases fall under the other's transform.  Rules: 0 the second half of the first
+// wave (blocks 256..511: the second slot of every CU if the dispatcher fills one per CU first), 1 the
+// odd blocks of the first wave, 2 every other block of an XCD (b & 8: blocks b and b + 8 share one).
+#ifndef C2_STAGGER
+#define C2_STAGGER 0
+#endif
+#ifndef C2_STAGGER_SEL
+#define C2_STAGGER_SEL 0
+#endif
+__device__ __forceinline__ void c2_stagger() {
+    if (C2_STAGGER <= 0) return;
+    const int b = blockIdx.x;
+    bool late;
+    if (C2_STAGGER_SEL == 0) late = b >= 256 && b < 512;
+    else if (C2_STAGGER_SEL == 1) late = b < 512 && (b & 1);
+    else late = b < 512 && (b & 8);
+    if (late)
+        for (int c = 0; c < C2_STAGGER; c += 8128) __builtin_amdgcn_s_sleep(127);
+}
+
 // exp(x / tau) as exp2(x * (log2 e / tau)): __expf lowers to a multiply by log2 e and v_exp_f32, so
 // with log2 e folded into the per-codeword scale every exponential is one instruction
 constexpr double C2_LOG2E = 1.4426950408889634074;
@@ -326,6 +358,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
     c2f *sMI = reinterpret_cast<c2f *>(smem + C2_IMG_BYTES);  // previous beta's (section max, 1 / sum)
     const int h = blockIdx.x & 1, cw = blockIdx.x >> 1, tid = threadIdx.x;
     if (!bf.active[cw]) return;
+    c2_stagger();
     const size_t lb = (size_t)cw * tb.L;
     for (int l = tid; l < tb.L; l += C2_T) {  // previous beta's section max, 1/sum
         sMI[l] = c2f{bf.stM[lb + l], bf.stI[lb + l]};
@@ -349,6 +382,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
         for (int j = 0; j < OT; ++j) ka[j] = c2_ldu(rk, 4 * tl, 4 * j * C2_T);
     };
     auto accumulate = [&](int m, const uint32_t *ka) {
+        if (C2_SKIP(2)) return;
 #pragma unroll
         for (int j = 0; j < OT; ++j) {
             const uint32_t a = ka[j] & CW_KMASK;
@@ -387,6 +421,11 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
             const __amdgpu_buffer_rsrc_t re = c2_rsrc(tb.cls2 + (size_t)m2 * CW2_SLICE, 4 * CW2_SLICE);
 #pragma unroll
             for (int i = 0; i < C2_SN; ++i) {
+                if (C2_SKIP(4)) {  // (synthetic entries inside the image, section 0)
+                    v[i] = (float)(tl + i);
+                    e[i] = (uint32_t)(((tl * 37 + i * 4099) & 8191) * 2);
+                    continue;
+                }
                 v[i] = c2_ldf(rs0, 4 * tl + 4 * i * C2_T, 0);
                 e[i] = c2_ldu(re, 4 * tl, 4 * i * C2_T);
             }
@@ -415,7 +454,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
         }
         __syncthreads();
         C2_TPC(3);
-        c2_fft<false>(tl, cmk);
+        if (!C2_SKIP(1)) c2_fft<false>(tl, cmk);
         C2_TPC(6);
     }
     {
@@ -543,6 +582,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
     float *dr = reinterpret_cast<float *>(smem);
     const int h = blockIdx.x & 1, cw = blockIdx.x >> 1, tid = threadIdx.x;
     if (!bf.active[cw]) return;
+    c2_stagger();
     const size_t lb = (size_t)cw * tb.L;
     const bool have_beta = t > 0;
     const double tv = bf.tau[cw];
@@ -581,11 +621,16 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
             const __amdgpu_buffer_rsrc_t re = c2_rsrc(tb.cls2 + (size_t)m2 * CW2_SLICE, 4 * CW2_SLICE);
 #pragma unroll
             for (int i = 0; i < C2_SN; ++i) {
+                if (C2_SKIP(128)) {  // (synthetic entries inside the image, section 0)
+                    v[i] = (float)(tl + i);
+                    e[i] = (uint32_t)(((tl * 37 + i * 4099) & 8191) * 2);
+                    continue;
+                }
                 e[i] = c2_ldu(re, 4 * tl, 4 * i * C2_T);
                 v[i] = c2_ldf(rs, 4 * tl + 4 * i * C2_T, 0);  // (t = 0: unused)
             }
         };
-        {  // rows r and P - r of each owned pair: sum of al v conj(W) / be v W over its outputs (v = z / phi),
+        if (!C2_SKIP(16)) {  // rows r and P - r of each owned pair: sum of al v conj(W) / be v W over its outputs (v = z / phi),
            // branch-free: every slot accumulates (NEWROW restarts the sums) and writes both rows, at the
            // addresses of the host table wab -- the pair's rows on its last slot, the trash slot otherwise
            // (invalid slots: al = be = 0); the two pairs whose rows coincide (r = 0, P / 2) then write their
@@ -605,6 +650,14 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
 #pragma unroll
                 for (int i = 0; i < CH; ++i) {
                     const int j = j0 + i < OT ? j0 + i : OT - 1;
+                    if (C2_SKIP(32)) {
+                        const uint32_t r = (uint32_t)(tl * 8 + j) & 4095u;
+                        ka[i] = r | CW_VALID | ((j & 1) ? CW_ENDROW : CW_NEWROW);
+                        gc[i] = make_float4(0.5f, 0.25f, 0.125f, 0.75f);
+                        vv[i] = (float)j;
+                        wa[i] = make_uint2(8u * (uint32_t)c2pos((int)r), 8u * (uint32_t)c2pos(8192 - (int)r));
+                        continue;
+                    }
                     ka[i] = c2_ldu(rk, 4 * tl, 4 * j * C2_T);
                     gc[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, 16 * tl, 16 * j * C2_T, 0));
                     vv[i] = c2_ldf(rv, 4 * tl, 4 * j * C2_T);
@@ -642,7 +695,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
         C2_TPC(33);
         __syncthreads();
         C2_TPC(34);
-        c2_fft<true>(tl, rmk);
+        if (!C2_SKIP(8)) c2_fft<true>(tl, rmk);
         C2_TPC(35);
         float snv[C2_SN];
         if constexpr (!EARLY) load_slice();
@@ -662,6 +715,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
         C2_TPC(37);
         __syncthreads();
         C2_TPC(38);
+        if (!C2_SKIP(64)) {
 #pragma unroll
         for (int c = 0; c < C2_SN; ++c) dr[tl + c * C2_T] = snv[c];  // s of the class in class order (past the
                                                                      // end: unread)
@@ -737,6 +791,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
             }
             if (jt[k] >= q0 && jt[k] < q1) st[k] = dr[jt[k] - q0];
         }
+        }  // (C2_SKIP(64))
         C2_TPC(40);
         __syncthreads();  // the next class overwrites the image
         C2_TPC(41);
@@ -807,7 +862,7 @@ __global__ __launch_bounds__(1024) void cw2_merge(Cw2Tables tb, RegBufs<float> b
         *psi = pnew;
         nmse[t + 1] = er / denom;
         bool stop = false;
-        if (t > 0) {
+        if (t > 0 && C2_ABL == 0) {  // (ablation builds never stop early: every launch does the same work)
             const double pp = *psi_prev;
             stop = fabs(pnew - pp) <= pr.atol + pr.rtol * fabs(pp);  // sparc.py:984-986
         }

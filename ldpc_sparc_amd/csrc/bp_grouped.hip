@@ -39,6 +39,9 @@ namespace sg {
 // terms of it still sum to a finite float, so no inf - inf reaches the
 // variable pass from the input.
 constexpr float GRP_CH_MAX = 1e30f;
+#ifndef BPG_SETUP_BATCH
+#define BPG_SETUP_BATCH 0
+#endif
 
 // LDS words addressed by their byte address.  The kernel has no static LDS
 // (grouped_one checks), so its dynamic image starts at address 0 and the
@@ -55,8 +58,12 @@ __device__ __forceinline__ lds_f32 *ldsf(uint32_t byte) { return (lds_f32 *)(siz
 // F2: first2 holds the slot addresses of the first two ports (low, high half)
 // in a register for the whole decode, so a degree-2 group reads no table at
 // all (the <4, 2> kernel; at <8, 4> the eight registers would spill)
+// init: the first iteration, whose incoming messages are all zero (the
+// reference starts from zero messages): nothing is read and the same sums of
+// zeros are formed (acc = ch + 0 + ... turns a -0 channel value into +0, as
+// the reference's does), so the image needs no zeroing before a codeword.
 template <int D, bool F2>
-__device__ __forceinline__ float grp_var(const uint16_t *gtab, float acc, uint32_t first2) {
+__device__ __forceinline__ float grp_var(const uint16_t *gtab, float acc, uint32_t first2, bool init) {
     if constexpr (D == 0) {
         return acc;
     } else {
@@ -65,8 +72,13 @@ __device__ __forceinline__ float grp_var(const uint16_t *gtab, float acc, uint32
 #pragma unroll
         for (int k = 0; k < D; ++k)
             sl[k] = (F2 && k == 0) ? (first2 & 0xffffu) : (F2 && k == 1) ? (first2 >> 16) : (uint32_t)gtab[64 * k];
+        if (init) {  // (uniform)
 #pragma unroll
-        for (int k = 0; k < D; ++k) m[k] = *ldsf(sl[k]);
+            for (int k = 0; k < D; ++k) m[k] = 0.0f;
+        } else {
+#pragma unroll
+            for (int k = 0; k < D; ++k) m[k] = *ldsf(sl[k]);
+        }
 #pragma unroll
         for (int k = 0; k < D; ++k) acc += m[k];
 #pragma unroll
@@ -81,7 +93,7 @@ __device__ __forceinline__ float grp_var(const uint16_t *gtab, float acc, uint32
 // ports in the reference's order.
 template <int D, bool F2>
 __device__ __forceinline__ void grp_var2(const uint16_t *gt0, const uint16_t *gt1, float &acc0, float &acc1,
-                                         uint32_t f0, uint32_t f1) {
+                                         uint32_t f0, uint32_t f1, bool init) {
     uint32_t s0[D], s1[D];
     float m0[D], m1[D];
 #pragma unroll
@@ -89,10 +101,15 @@ __device__ __forceinline__ void grp_var2(const uint16_t *gt0, const uint16_t *gt
         s0[k] = (F2 && k == 0) ? (f0 & 0xffffu) : (F2 && k == 1) ? (f0 >> 16) : (uint32_t)gt0[64 * k];
         s1[k] = (F2 && k == 0) ? (f1 & 0xffffu) : (F2 && k == 1) ? (f1 >> 16) : (uint32_t)gt1[64 * k];
     }
+    if (init) {  // (uniform)
 #pragma unroll
-    for (int k = 0; k < D; ++k) {
-        m0[k] = *ldsf(s0[k]);
-        m1[k] = *ldsf(s1[k]);
+        for (int k = 0; k < D; ++k) m0[k] = m1[k] = 0.0f;
+    } else {
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            m0[k] = *ldsf(s0[k]);
+            m1[k] = *ldsf(s1[k]);
+        }
     }
 #pragma unroll
     for (int k = 0; k < D; ++k) {
@@ -108,12 +125,12 @@ __device__ __forceinline__ void grp_var2(const uint16_t *gt0, const uint16_t *gt
 
 template <bool F2>
 __device__ __forceinline__ void grp_var2_d(int d, const uint16_t *gt0, const uint16_t *gt1, float &acc0,
-                                           float &acc1, uint32_t f0, uint32_t f1) {
+                                           float &acc1, uint32_t f0, uint32_t f1, bool init) {
     static_assert(GRP_PAIR_MAXD == 3, "pair degrees");
     switch (d) {
-        case 1: grp_var2<1, F2>(gt0, gt1, acc0, acc1, f0, f1); break;
-        case 2: grp_var2<2, F2>(gt0, gt1, acc0, acc1, f0, f1); break;
-        case 3: grp_var2<3, F2>(gt0, gt1, acc0, acc1, f0, f1); break;
+        case 1: grp_var2<1, F2>(gt0, gt1, acc0, acc1, f0, f1, init); break;
+        case 2: grp_var2<2, F2>(gt0, gt1, acc0, acc1, f0, f1, init); break;
+        case 3: grp_var2<3, F2>(gt0, gt1, acc0, acc1, f0, f1, init); break;
         default: break;  // (the host pairs degrees 1..GRP_PAIR_MAXD only)
     }
 }
@@ -149,9 +166,9 @@ __device__ __forceinline__ uint32_t grp_check(uint32_t addr, float factor, uint3
 
 // uniform (per-wave) degree dispatch
 template <bool F2>
-__device__ __forceinline__ float grp_var_d(int d, const uint16_t *gtab, float acc, uint32_t first2) {
+__device__ __forceinline__ float grp_var_d(int d, const uint16_t *gtab, float acc, uint32_t first2, bool init) {
     switch (d) {
-#define SG_GV(N) case N: return grp_var<N, F2>(gtab, acc, first2);
+#define SG_GV(N) case N: return grp_var<N, F2>(gtab, acc, first2, init);
         SG_GV(0) SG_GV(1) SG_GV(2) SG_GV(3) SG_GV(4) SG_GV(5) SG_GV(6) SG_GV(7) SG_GV(8)
         SG_GV(9) SG_GV(10) SG_GV(11) SG_GV(12) SG_GV(13) SG_GV(14) SG_GV(15) SG_GV(16)
 #undef SG_GV
@@ -216,39 +233,68 @@ __global__ __launch_bounds__(BP_THREADS, VJ <= 4 ? 8 : 6) void bp_grouped_minsum
     }
     const float factor = a.factor;
     const uint32_t fsign = __float_as_uint(factor) & 0x80000000u;
-    const int nwords = a.msg_bytes / 4;
     for (int cw = blockIdx.x; cw < a.B; cw += gridDim.x) {
         const float *ch = a.ch + (size_t)cw * a.nv;
         float chv[VJ], apv[VJ];
+        {
+            // the lanes' variables, then their channel values, each in one round of loads (padding lanes read
+            // variable 0 and drop it); the zero offset is opaque so the codeword-invariant index loads are not
+            // hoisted out of the codeword loop (live across the decode they would not fit the 64 VGPRs)
+            int zo = 0;
+            asm volatile("" : "+v"(zo));
+#if BPG_SETUP_BATCH
+            // raw buffer loads, no branch: a padding lane (variable -1) reads past the buffer's end, which the
+            // hardware range check returns as 0
+            const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<int32_t *>(a.vmap + wave * VJ * 64), 0, 4 * 64 * VJ, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(ch), 0,
+                                                                                4 * a.nv, 0x00020000);
+            int v[VJ];
 #pragma unroll
-        for (int j = 0; j < VJ; ++j) {
-            const int v = j < a.vj ? vmap[64 * j] : -1;
-            // saturated at +-GRP_CH_MAX (and inf with it): the kernel is built
-            // without NaN semantics, and a sum of saturated inputs stays finite
-            chv[j] = v >= 0 ? __builtin_amdgcn_fmed3f(ch[v], -GRP_CH_MAX, GRP_CH_MAX) : 0.0f;
-            apv[j] = 0.0f;
+            for (int j = 0; j < VJ; ++j)
+                v[j] = j < a.vj ? (int)__builtin_amdgcn_raw_buffer_load_b32(rm, 4 * (lane + zo), 4 * 64 * j, 0) : -1;
+#pragma unroll
+            for (int j = 0; j < VJ; ++j) {
+                // saturated at +-GRP_CH_MAX (and inf with it): the kernel is built
+                // without NaN semantics, and a sum of saturated inputs stays finite
+                const float x = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, 4 * v[j], 0, 0));
+                chv[j] = __builtin_amdgcn_fmed3f(x, -GRP_CH_MAX, GRP_CH_MAX);
+                apv[j] = 0.0f;
+            }
+#else
+#pragma unroll
+            for (int j = 0; j < VJ; ++j) {
+                const int v = j < a.vj ? vmap[64 * j + zo] : -1;
+                chv[j] = v >= 0 ? __builtin_amdgcn_fmed3f(ch[v], -GRP_CH_MAX, GRP_CH_MAX) : 0.0f;
+                apv[j] = 0.0f;
+            }
+#endif
         }
-        for (int i = tid; i < nwords; i += BP_THREADS) reinterpret_cast<float *>(smem)[i] = 0.0f;
-        __syncthreads();
-        int it = 0;
-        for (; it < a.max_it; ++it) {
-            // ---- variable pass (c_ldpc.c:171-178): groups 2i and 2i + 1 as a pair
-            // when the host flagged one (pairs sit at even positions)
+        // ---- variable pass (c_ldpc.c:171-178): groups 2i and 2i + 1 as a pair
+        // when the host flagged one (pairs sit at even positions)
+        auto var_pass = [&](bool init) {
 #pragma unroll
             for (int j = 0; j < VJ; j += 2) {
                 if (j >= a.vj) continue;
                 if (vpair[j]) {
                     float a0 = chv[j], a1 = chv[j + 1];
                     grp_var2_d<F2>(vd[j], a.vtab + vt[j] + lane, a.vtab + vt[j + 1] + lane, a0, a1, first2[j],
-                                   first2[j + 1]);
+                                   first2[j + 1], init);
                     apv[j] = a0;
                     apv[j + 1] = a1;
                 } else {
-                    apv[j] = grp_var_d<F2>(vd[j], a.vtab + vt[j] + lane, chv[j], first2[j]);
-                    if (j + 1 < a.vj) apv[j + 1] = grp_var_d<F2>(vd[j + 1], a.vtab + vt[j + 1] + lane, chv[j + 1],
-                                                                first2[j + 1]);
+                    apv[j] = grp_var_d<F2>(vd[j], a.vtab + vt[j] + lane, chv[j], first2[j], init);
+                    if (j + 1 < a.vj)
+                        apv[j + 1] = grp_var_d<F2>(vd[j + 1], a.vtab + vt[j + 1] + lane, chv[j + 1], first2[j + 1],
+                                                   init);
                 }
             }
+        };
+        // (the previous codeword's last reads of the image and of the flags are behind the barrier that
+        // ended it)
+        int it = 0;
+        for (; it < a.max_it; ++it) {
+            var_pass(it == 0);  // (the first: zero incoming messages, no reads, no zeroed image)
             __syncthreads();
             // ---- check pass (c_ldpc.c:183-194 with the min-sum update)
             uint32_t unsat = 0u;

@@ -35,6 +35,21 @@ struct GemmF32 {
 };
 
 constexpr int GBN = 128, GBK = 32, GPAD = GBK + 1;
+
+// The design-matrix operand (Y) is streamed once per launch; its loads can be
+// non-temporal so that its lines leave the XCD's L2 first and the batch
+// operand, which every N tile re-reads, stays resident (A/B: -DGEMM_Y_NT=0/1).
+#ifndef GEMM_Y_NT
+#define GEMM_Y_NT 0
+#endif
+__device__ __forceinline__ float4 gemm_ld_y(const float *p) {
+    if (GEMM_Y_NT) {
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
+        return make_float4(v.x, v.y, v.z, v.w);
+    }
+    return *reinterpret_cast<const float4 *>(p);
+}
 template <int MT>
 constexpr int gbm() { return 64 * MT; }
 
@@ -65,15 +80,13 @@ __global__ __launch_bounds__(256, MT == 4 ? 2 : 1) void gemm_f32_mfma(GemmF32 g)
             if (NT) {
                 const int r = f >> 3, c = (f & 7) * 4;
                 const int nn = n0 + r;
-                yr[p] = (nn < g.yrows && k0 + c < ke)
-                            ? *reinterpret_cast<const float4 *>(g.Y + (long)nn * g.ldy + k0 + c)
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
+                yr[p] = (nn < g.yrows && k0 + c < ke) ? gemm_ld_y(g.Y + (long)nn * g.ldy + k0 + c)
+                                                      : make_float4(0.f, 0.f, 0.f, 0.f);
             } else {
                 const int r2 = f >> 5, c2 = (f & 31) * 4;
                 const int kk = k0 + r2, nn = n0 + c2;
-                yr[p] = (kk < ke && kk < g.yrows && nn < g.N)
-                            ? *reinterpret_cast<const float4 *>(g.Y + (long)kk * g.ldy + nn)
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
+                yr[p] = (kk < ke && kk < g.yrows && nn < g.N) ? gemm_ld_y(g.Y + (long)kk * g.ldy + nn)
+                                                               : make_float4(0.f, 0.f, 0.f, 0.f);
             }
         }
     };
