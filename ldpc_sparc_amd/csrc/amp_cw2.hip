@@ -63,6 +63,17 @@ static_assert(C2_EPT == 16, "the transform is written for 16 values per thread")
 #ifndef C2_STAGGER
 #define C2_STAGGER 0
 #endif
+// Az statistics: the segment's reads unconditional (A/B); no argmax, the maximum's term dropped by fract (A/B)
+#ifndef C2_STATS_LOADS
+#define C2_STATS_LOADS 0
+#endif
+#ifndef C2_STATS_V2
+#define C2_STATS_V2 0
+#endif
+// Az rows: the row addresses from the slot's flags instead of the host table wab (A/B)
+#ifndef C2_ROWS_DERIVE
+#define C2_ROWS_DERIVE 0
+#endif
 #ifndef C2_STAGGER_SEL
 #define C2_STAGGER_SEL 0
 #endif
@@ -661,7 +672,8 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
                     ka[i] = c2_ldu(rk, 4 * tl, 4 * j * C2_T);
                     gc[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, 16 * tl, 16 * j * C2_T, 0));
                     vv[i] = c2_ldf(rv, 4 * tl, 4 * j * C2_T);
-                    wa[i] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rw, 8 * tl, 8 * j * C2_T, 0));
+                    if (!C2_ROWS_DERIVE)
+                        wa[i] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rw, 8 * tl, 8 * j * C2_T, 0));
                 }
 #pragma unroll
                 for (int j = 0; j < CH; ++j) {
@@ -671,6 +683,12 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
                     const float keep = (k & CW_NEWROW) ? 0.f : 1.f;
                     u0 = cmacc_pk({u0.x * keep, u0.y * keep}, {gc[j].x * vv[j], gc[j].y * vv[j]}, w);
                     u1 = cmac_pk({u1.x * keep, u1.y * keep}, {gc[j].z * vv[j], gc[j].w * vv[j]}, w);
+                    if (C2_ROWS_DERIVE) {  // the host table wab from the slot's flags: rows on the pair's last slot
+                        const int r = (int)(k & (uint32_t)(C2_P - 1)), rb = C2_P - r;
+                        const bool end = (k & CW_ENDROW) != 0;
+                        wa[j].x = end ? 8u * (uint32_t)c2pos(r) : 4u * CW2_TRASH;
+                        wa[j].y = (end && !(k & CW_SELF)) ? 8u * (uint32_t)c2pos(rb) : 4u * CW2_TRASH;
+                    }
                     c2lds *pa = (c2lds *)(size_t)wa[j].x, *pb = (c2lds *)(size_t)wa[j].y;
                     *pa = c2f{u0.x, u0.y};
                     *pb = c2f{u1.x, u1.y};
@@ -736,8 +754,68 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
             constexpr int RC = 16;
             const float *sgp = dr + a;  // inside the LDS image past the segment's end too
             float x[RC];
+#if C2_STATS_LOADS
+            // every read unconditional, the entries past the segment masked afterwards: written as
+            // `i < n ? sgp[i] : -inf` the compiler put each read in its own exec-masked block (two SALU
+            // mask operations per read, no paired reads)
+#pragma unroll
+            for (int i = 0; i < RC; ++i) x[i] = sgp[i];
+#pragma unroll
+            for (int i = 0; i < RC; ++i) {  // -inf past the segment by a sign mask and v_bfi (a compare and a
+                                            // select would serialise on one SGPR pair with hazard nops)
+                const uint32_t mk = (uint32_t)((i - n) >> 31);  // all ones inside the segment
+                x[i] = __uint_as_float((__float_as_uint(x[i]) & mk) | (0xff800000u & ~mk));
+            }
+#else
 #pragma unroll
             for (int i = 0; i < RC; ++i) x[i] = i < n ? sgp[i] : -INFINITY;
+#endif
+#if C2_STATS_V2
+            // no argmax: the maximum by a max3 tree; in the sums, v_fract_f32 drops the entries equal to the
+            // maximum (e = exp2(0) = 1 exactly, fract 0; below it e < 1, fract(e) = e) and the entries that
+            // tie with it are added back afterwards from Se - S1 = their count (exact small integers), so
+            // S1 = sum over every entry but one maximum, as before -- two mask operations fewer per entry
+            float m = x[0];
+#pragma unroll
+            for (int i = 1; i + 1 < RC; i += 2) m = fmaxf(fmaxf(m, x[i]), x[i + 1]);
+            if constexpr (RC % 2 == 0) m = fmaxf(m, x[RC - 1]);
+            for (int c = RC; c < n; c += RC) {
+                float y[RC];
+#pragma unroll
+                for (int i = 0; i < RC; ++i) y[i] = dr[a + c + i];
+#pragma unroll
+                for (int i = 0; i < RC; ++i) m = fmaxf(m, c + i < n ? y[i] : -INFINITY);
+            }
+            float S1 = 0.f, S2 = 0.f, Se = 0.f;
+#pragma unroll
+            for (int i = 0; i < RC; ++i) {
+                const float ex = c2_exp2((x[i] - m) * inv_tau);
+                const float f = __builtin_amdgcn_fractf(ex);
+                S1 += f;
+                S2 += f * f;
+                Se += ex;
+            }
+            for (int c = RC; c < n; c += RC) {
+                float y[RC];
+#pragma unroll
+                for (int i = 0; i < RC; ++i) y[i] = dr[a + c + i];
+#pragma unroll
+                for (int i = 0; i < RC; ++i) {
+                    const float ex = c2_exp2(((c + i < n ? y[i] : -INFINITY) - m) * inv_tau);
+                    const float f = __builtin_amdgcn_fractf(ex);
+                    S1 += f;
+                    S2 += f * f;
+                    Se += ex;
+                }
+            }
+            {
+                const float ties = rintf(Se - S1) - 1.f;  // entries equal to the maximum, but one (NaN: empty)
+                if (ties > 0.f) {
+                    S1 += ties;
+                    S2 += ties;
+                }
+            }
+#else
             float m = -INFINITY;
             int am = -1;
 #pragma unroll
@@ -777,6 +855,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
                     S2 += ex * ex;
                 }
             }
+#endif
             if (m > -INFINITY) {  // merge into the section's running statistics
                 if (m > Mr[k]) {
                     const float f = c2_exp2((Mr[k] - m) * inv_tau);

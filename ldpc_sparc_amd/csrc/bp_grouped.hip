@@ -39,6 +39,10 @@ namespace sg {
 // terms of it still sum to a finite float, so no inf - inf reaches the
 // variable pass from the input.
 constexpr float GRP_CH_MAX = 1e30f;
+// two check groups of one degree in a wave run together (A/B: -DBPG_CHECK_PAIRS=0)
+#ifndef BPG_CHECK_PAIRS
+#define BPG_CHECK_PAIRS 1
+#endif
 #ifndef BPG_SETUP_BATCH
 #define BPG_SETUP_BATCH 0
 #endif
@@ -162,6 +166,56 @@ __device__ __forceinline__ uint32_t grp_check(uint32_t addr, float factor, uint3
         c[64 * k] = __uint_as_float(((__float_as_uint(L[k]) ^ Sf) & 0x80000000u) | mag);
     }
     return unsat;
+}
+
+// Two check groups of one degree DC together: both groups' LDS reads in flight
+// at once, then both updates (one chain of round trips for the pair).  Each
+// check's update is grp_check's, operation for operation.
+template <int DC>
+__device__ __forceinline__ uint32_t grp_check2(uint32_t addr0, uint32_t addr1, float factor, uint32_t fsign,
+                                               bool valid0, bool valid1) {
+    float L0[DC], L1[DC];
+    lds_f32 *c0 = ldsf(addr0), *c1 = ldsf(addr1);
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        L0[k] = c0[64 * k];
+        L1[k] = c1[64 * k];
+    }
+    uint32_t u = 0u;
+    auto upd = [&](float *L, lds_f32 *c, bool valid) {
+        float m1 = INFINITY, m2 = INFINITY;
+        uint32_t S = 0u;
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+            const float a = fabsf(L[k]);
+            m2 = __builtin_amdgcn_fmed3f(a, m1, m2);
+            m1 = fminf(m1, a);
+            S ^= __float_as_uint(L[k]);
+        }
+        const uint32_t unsat = (S >> 31) | (m1 > 0.0f ? 0u : 1u);
+        uint32_t b1 = __float_as_uint(m1 * factor) & 0x7fffffffu, b2 = __float_as_uint(m2 * factor) & 0x7fffffffu;
+        asm volatile("" : "+v"(b1), "+v"(b2));
+        const uint32_t Sf = S ^ fsign;
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+            const uint32_t mag = fabsf(L[k]) == m1 ? b2 : b1;
+            c[64 * k] = __uint_as_float(((__float_as_uint(L[k]) ^ Sf) & 0x80000000u) | mag);
+        }
+        u |= valid ? unsat : 0u;
+    };
+    upd(L0, c0, valid0);
+    upd(L1, c1, valid1);
+    return u;
+}
+
+__device__ __forceinline__ uint32_t grp_check2_d(int d, uint32_t a0, uint32_t a1, float f, uint32_t fs, bool v0,
+                                                 bool v1) {
+    switch (d) {
+#define SG_GC2(N) case N: return grp_check2<N>(a0, a1, f, fs, v0, v1);
+        SG_GC2(2) SG_GC2(3) SG_GC2(4) SG_GC2(5) SG_GC2(6) SG_GC2(7)
+#undef SG_GC2
+        default: return 0u;
+    }
 }
 
 // uniform (per-wave) degree dispatch
@@ -299,11 +353,20 @@ __global__ __launch_bounds__(BP_THREADS, VJ <= 4 ? 8 : 6) void bp_grouped_minsum
             // ---- check pass (c_ldpc.c:183-194 with the min-sum update)
             uint32_t unsat = 0u;
 #pragma unroll
-            for (int q = 0; q < CJ; ++q)
-                if (q < a.cj) {
+            for (int q = 0; q < CJ; q += 2) {
+                if (q >= a.cj) continue;
+                if (BPG_CHECK_PAIRS && q + 1 < a.cj && cdg[q + 1] == cdg[q] && cdg[q] <= 7) {  // (uniform; degree 8 pairs spill)
+                    unsat |= grp_check2_d(cdg[q], ca[q] + 4 * lane, ca[q + 1] + 4 * lane, factor, fsign,
+                                          lane < cn[q], lane < cn[q + 1]);
+                } else {
                     const uint32_t u = grp_check_d(cdg[q], ca[q] + 4 * lane, factor, fsign);
                     unsat |= lane < cn[q] ? u : 0u;
+                    if (q + 1 < a.cj) {
+                        const uint32_t u1 = grp_check_d(cdg[q + 1], ca[q + 1] + 4 * lane, factor, fsign);
+                        unsat |= lane < cn[q + 1] ? u1 : 0u;
+                    }
                 }
+            }
             // ---- stop when every check is satisfied (c_ldpc.c:196-197): one
             // flag per wave, parity-buffered (this iteration's words were last
             // read before the previous iteration's variable-pass barrier)
