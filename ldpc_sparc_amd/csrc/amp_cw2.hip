@@ -65,14 +65,14 @@ static_assert(C2_EPT == 16, "the transform is written for 16 values per thread")
 #endif
 // Az statistics: the segment's reads unconditional (A/B); no argmax, the maximum's term dropped by fract (A/B)
 #ifndef C2_STATS_LOADS
-#define C2_STATS_LOADS 0
+#define C2_STATS_LOADS 1
 #endif
 #ifndef C2_STATS_V2
-#define C2_STATS_V2 0
+#define C2_STATS_V2 1
 #endif
 // Az rows: the row addresses from the slot's flags instead of the host table wab (A/B)
 #ifndef C2_ROWS_DERIVE
-#define C2_ROWS_DERIVE 0
+#define C2_ROWS_DERIVE 1
 #endif
 #ifndef C2_STAGGER_SEL
 #define C2_STAGGER_SEL 0
@@ -317,9 +317,18 @@ __device__ __forceinline__ void c2_fft(int tid, uint32_t msk) {
 
 // diagnostics (SG_AMP_TPROF): thread 0 stamps the shader clock at point k of
 // the half's third class (cw2_ab: 0-15, cw2_az: 32-47) and at kernel entry / exit
+// (compiled in only with the stamps: -DC2_STAMPS=1, or a diagnostic build `make DIAG=1`; in the shipped
+// build each point's runtime test cost about five scalar instructions per class and stamp point)
+#if !defined(C2_STAMPS) && defined(SG_DIAG)
+#define C2_STAMPS 1
+#endif
+#ifndef C2_STAMPS
+#define C2_STAMPS 0
+#endif
 #define C2_TP(k)                                                                                                \
     do {                                                                                                        \
-        if (tb.tprof && threadIdx.x == 0) tb.tprof[(size_t)blockIdx.x * 64 + (k)] = __builtin_readcyclecounter(); \
+        if (C2_STAMPS && tb.tprof && threadIdx.x == 0)                                                          \
+            tb.tprof[(size_t)blockIdx.x * 64 + (k)] = __builtin_readcyclecounter();                             \
     } while (0)
 #define C2_TPC(k)                          \
     do {                                   \
@@ -642,10 +651,10 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
             }
         };
         if (!C2_SKIP(16)) {  // rows r and P - r of each owned pair: sum of al v conj(W) / be v W over its outputs (v = z / phi),
-           // branch-free: every slot accumulates (NEWROW restarts the sums) and writes both rows, at the
-           // addresses of the host table wab -- the pair's rows on its last slot, the trash slot otherwise
-           // (invalid slots: al = be = 0); the two pairs whose rows coincide (r = 0, P / 2) then write their
-           // sum.  (a, al, be, v and the addresses reloaded per class from L1 / L2: held across the transform,
+           // branch-free: every slot accumulates (NEWROW restarts the sums) and writes both rows -- the
+           // pair's rows on its last slot (ENDROW), the trash slot otherwise (invalid slots: al = be = 0),
+           // addresses derived from the slot word (C2_ROWS_DERIVE; the host table wab is the A/B form) --
+           // the two pairs whose rows coincide (r = 0, P / 2) then write their sum.  (a, al, be, v and the addresses reloaded per class from L1 / L2: held across the transform,
            // or loaded one class ahead, they spill; al v and be v precomputed per codeword were slower -- four
            // times the per-codeword bytes re-read from L2 every class.)
             constexpr int CH = OT > 12 ? (OT + 1) / 2 : OT;  // slots per load round (one round at 12 per thread)
@@ -741,15 +750,18 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
         C2_TPC(39);
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
-            // partial of the section over its segment: the maximum and its first
-            // position, then the sums of e and e^2 over the other entries
-            // (e = exp((x - max) / tau)); two passes with selects instead of the
-            // online rescaling (fewer vector instructions).  The first 16
-            // entries are read once for both passes (segments average
-            // LM / (Q L) = 8 entries; longer ones take the loops below), the
-            // reads are unskewed (every read a base plus a constant; the
-            // segment starts are irregular either way) and entries past the
-            // segment read as -inf (exp -> 0).
+            // partial of the section over its segment: the maximum, then the
+            // sums of e and e^2 over every entry but one maximum
+            // (e = exp((x - max) / tau)); two passes instead of the online
+            // rescaling (fewer vector instructions).  The first 16 entries are
+            // read once for both passes (segments average LM / (Q L) = 8
+            // entries; longer ones take the loops below), the reads are
+            // unskewed (every read a base plus a constant; the segment starts
+            // are irregular either way) and entries past the segment are -inf
+            // (exp -> 0).  Same box, every codeword active (tools/c2_ablate.py,
+            // profiles/r05_c2_variants.txt): the statistics were 28 % of
+            // cw2_az; unconditional reads, the fract form below and the rows'
+            // derived addresses took cw2_az 0.588 -> 0.570 ms per launch.
             const int a = sa[k], n = sb[k] - sa[k];
             constexpr int RC = 16;
             const float *sgp = dr + a;  // inside the LDS image past the segment's end too

@@ -2,7 +2,9 @@
 (amp_cw2.hip C2_TP points, SG_AMP_TPROF): one C2 batch decode (bench design,
 B = 256), then the mean / max cycles between the stamps of the last
 iteration's third class of every workgroup half, and the kernels' per-class
-cycles (entry to exit over the half's classes)."""
+cycles (entry to exit over the half's classes).  The stamps are compiled in
+only in a diagnostic library (make -C ldpc_sparc_amd/csrc DIAG=1, or a variant
+built with -DC2_STAMPS=1 loaded through LDPC_SPARC_AMD_LIB)."""
 import ctypes as ct
 import os
 import sys
