@@ -48,7 +48,8 @@ static_assert(C2_EPT == 16, "the transform is written for 16 values per thread")
 // Phase ablation for timing studies only (tools/c2_ablate.py on variants built by
 // tools/mk_variant.sh with -DC2_ABL=<mask>; results are garbage, the shipped build has 0):
 // 1 Ab FFT, 2 Ab accumulation, 4 Ab slice loads, 8 Az FFT, 16 Az rows, 32 Az rows' table
-// loads (values from the thread index), 64 Az statistics + class copy, 128 Az slice loads
+// loads (values from the thread index), 64 Az statistics + class copy, 128 Az slice loads, 256 Ab scatter,
+// 512 Ab beta stores, 1024 Az gathers from the image
 #ifndef C2_ABL
 #define C2_ABL 0
 #endif
@@ -466,7 +467,8 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
                 const int sec = e[i] >> 16;
                 const c2f mi = sMI[sec];
                 v[i] = c2_exp2((v[i] - mi.x) * inv_tp) * mi.y;
-                dr[e[i] & 0xffffu] = v[i];
+                if (!C2_SKIP(256)) dr[e[i] & 0xffffu] = v[i];
+                if (!C2_SKIP(512))
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[i]), rs, 4 * tl + 4 * i * C2_T,
                                                       0, 0);
             }
@@ -730,7 +732,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
 #pragma unroll
             for (int i = 0; i < C2_SN; ++i) {  // s = beta_prev + tau u (sparc.py:972); beta_prev stored by cw2_ab
                 const float b = have_beta ? v[i] : 0.f;
-                snv[i] = b + tau * dr[e[i] & 0xffffu];
+                snv[i] = b + tau * (C2_SKIP(1024) ? (float)i : dr[e[i] & 0xffffu]);
             }
         }
         C2_TPC(36);

@@ -39,9 +39,10 @@ namespace sg {
 // terms of it still sum to a finite float, so no inf - inf reaches the
 // variable pass from the input.
 constexpr float GRP_CH_MAX = 1e30f;
-// two check groups of one degree in a wave run together (A/B: -DBPG_CHECK_PAIRS=0)
+// two check groups of one degree in a wave run together (A/B: -DBPG_CHECK_PAIRS=1; same box within noise,
+// profiles/r05_bp_ab.txt, and it spills a VGPR in the codeword loop: off)
 #ifndef BPG_CHECK_PAIRS
-#define BPG_CHECK_PAIRS 1
+#define BPG_CHECK_PAIRS 0
 #endif
 #ifndef BPG_SETUP_BATCH
 #define BPG_SETUP_BATCH 0

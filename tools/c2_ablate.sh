@@ -7,7 +7,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/abl; rm -rf $O; mkdir -p $O
 for i in 1 2; do
   timeout -k 10 120 python tools/c2_ablate.py 256 10 3 >> $O/cur.jsonl 2>> $O/err.log
-  for d in ldpc_sparc_amd/_lib_v_abl* ldpc_sparc_amd/_lib_v_nosst; do
+  for d in ldpc_sparc_amd/_lib_v_abl*; do
     n=${d#ldpc_sparc_amd/_lib_v_}
     LDPC_SPARC_AMD_LIB=$PWD/$d/libldpc_sparc_amd.so timeout -k 10 120 python tools/c2_ablate.py 256 10 3 >> $O/$n.jsonl 2>> $O/err.log
     echo "$i $n" 
