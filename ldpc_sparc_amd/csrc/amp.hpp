@@ -207,11 +207,14 @@ __host__ __device__ constexpr int c2pos(int i) { return i + (i >> 5); }
 constexpr uint32_t CW2_TRASH = 2 * (8192 + 256) + 2048;  // LDS float index of the trash slot (after the
                                                          // padded image and the statistics)
 constexpr uint32_t CW_SELF = 1u << 23;  // the pair's two rows coincide (r = 0 or P / 2)
+// a thread's slots padded to a multiple of four (thread-major tables: 16-byte loads)
+__host__ __device__ constexpr int cw2_otp(int ot) { return (ot + 3) & ~3; }
 struct Cw2Tables {
     int L, M, LM, n, N2, Q, Lblk, OT, maxcls;
     float inv_n2;             // 1 / N2
     const uint32_t *cmask;    // [Q + 1][512] image values each thread's first FFT stage reads (class m2; rows: Q)
     const uint32_t *ka;       // [OT][512] a | CW_VALID | CW_NEWROW (first of its pair) | CW_ENDROW | CW_SELF
+    const uint32_t *kat;      // [512][OTP] the same, thread-major (a thread's slots in 16-byte loads)
     const int32_t *oi;        // [OT][512] output index (invalid slots: 0)
     const float4 *cf;         // [OT][512] (c1, c2): output = Re(c1 H[a] + c2 conj H[N2 - a])
     const float4 *gf;         // [OT][512] (al, be): G[a] += al z/phi, G[N2 - a] += be z/phi
@@ -224,7 +227,7 @@ struct Cw2Tables {
     const uint2 *rab;         // [OT][512] LDS byte addresses of rows r, P - r of the slot's output (cw2_ab reads)
     const uint2 *wab;         // [OT][512] LDS byte addresses of the slot's row writes (rows r, P - r on the
                               // pair's last slot, else the trash slot; r = 0, P / 2: row r and trash)
-    float *vz;                // [B][OT][512] z / phi in slot order
+    float *vz;                // [B][512][OTP] z / phi in slot order, thread-major (OTP = OT rounded up to 4)
     float *ys, *zs;           // [B][OT][512] y (copied at t = 0) and z in slot order (cw2_ctrl reads them
                               // coalesced; z in natural order is still written for a hand-over)
     float4 *part;             // [B][2][Lblk] partial section statistics (max, R1, R2, s of the true entry or NaN)

@@ -369,6 +369,18 @@ __device__ __forceinline__ uint32_t c2_ldu(__amdgpu_buffer_rsrc_t r, int vo, int
 // workgroup-uniform values (class bounds) in scalar registers: a buffer
 // resource built from them stays scalar (no waterfall loop)
 __device__ __forceinline__ int c2_uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+// a thread's OT slot words of a thread-major [512][OTP] table, 16 bytes per load
+template <int OT>
+__device__ __forceinline__ void c2_ld_slots(__amdgpu_buffer_rsrc_t r, int tl, uint32_t *out) {
+    constexpr int OTP = cw2_otp(OT);
+#pragma unroll
+    for (int q = 0; q < OTP / 4; ++q) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, 4 * OTP * tl, 16 * q, 0);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            if (4 * q + c < OT) out[4 * q + c] = v[c];
+    }
+}
 constexpr int C2_SN = C2_NC * C2_SC;  // class entries per thread
 
 
@@ -397,10 +409,10 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
     // H[a] += W Y[r], conj H[b] += W conj Y[P - r] from the image's transform of class m (invalid slots:
     // a = 0, unused); the owned indices a and the rows' LDS byte addresses (host table rab) reloaded per
     // class from L1 (held across the transform they spill), in two rounds
-    const __amdgpu_buffer_rsrc_t rk = c2_rsrc(tb.ka, 4 * OT * C2_T);
+    constexpr int OTP = cw2_otp(OT);
+    const __amdgpu_buffer_rsrc_t rk = c2_rsrc(tb.kat, 4 * OTP * C2_T);  // thread-major: OTP / 4 loads of 16 B
     auto acc_tables = [&](int tl, uint32_t *ka) {
-#pragma unroll
-        for (int j = 0; j < OT; ++j) ka[j] = c2_ldu(rk, 4 * tl, 4 * j * C2_T);
+        c2_ld_slots<OT>(rk, tl, ka);
     };
     auto accumulate = [&](int m, const uint32_t *ka) {
         if (C2_SKIP(2)) return;
@@ -592,9 +604,15 @@ __global__ __launch_bounds__(C2_T) void cw2_ctrl(Cw2Tables tb, RegBufs<float> bf
         bf.tau[cw] = tv_new;
     }
     const float iph = (float)(1.0 / phi);
-    float *vz = tb.vz + (size_t)cw * OT * C2_T;
+    constexpr int OTP = cw2_otp(OT);
+    float4 *vz4 = reinterpret_cast<float4 *>(tb.vz + ((size_t)cw * C2_T + tid) * OTP);  // thread-major
 #pragma unroll
-    for (int j = 0; j < OT; ++j) vz[j * C2_T + tid] = zr[j] * iph;  // z / phi (sparc.py:972)
+    for (int q = 0; q < OTP / 4; ++q) {  // z / phi (sparc.py:972); padding slots 0
+        float w[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) w[c] = 4 * q + c < OT ? zr[4 * q + c] * iph : 0.f;
+        vz4[q] = make_float4(w[0], w[1], w[2], w[3]);
+    }
 }
 
 // ---------------------------------------------------------------------------- Az
@@ -610,7 +628,8 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
     const double tv = bf.tau[cw];
     const float tau = (float)tv, inv_tau = (float)(C2_LOG2E / tv);  // log2 e / tau (c2_exp2)
     float *s = bf.s + (size_t)cw * tb.LM;
-    const float *vz = tb.vz + (size_t)cw * OT * C2_T;
+    constexpr int OTP = cw2_otp(OT);
+    const float *vz = tb.vz + (size_t)cw * OTP * C2_T;  // [512][OTP] thread-major
     // running statistics of sections tid and tid + 512 over this half's classes
     const int Lb = tb.Lblk;
     float Mr[2] = {-INFINITY, -INFINITY}, R1[2] = {0.f, 0.f}, R2[2] = {0.f, 0.f}, st[2] = {NAN, NAN};
@@ -660,8 +679,16 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
            // or loaded one class ahead, they spill; al v and be v precomputed per codeword were slower -- four
            // times the per-codeword bytes re-read from L2 every class.)
             constexpr int CH = OT > 12 ? (OT + 1) / 2 : OT;  // slots per load round (one round at 12 per thread)
-            const __amdgpu_buffer_rsrc_t rg = c2_rsrc(tb.gf, 16 * OT * C2_T), rv = c2_rsrc(vz, 4 * OT * C2_T),
-                                         rk = c2_rsrc(tb.ka, 4 * OT * C2_T), rw = c2_rsrc(tb.wab, 8 * OT * C2_T);
+            const __amdgpu_buffer_rsrc_t rg = c2_rsrc(tb.gf, 16 * OT * C2_T), rv = c2_rsrc(vz, 4 * OTP * C2_T),
+                                         rk = c2_rsrc(tb.kat, 4 * OTP * C2_T), rw = c2_rsrc(tb.wab, 8 * OT * C2_T);
+            // one load round (CH == OT): a thread's slot words and z / phi in 16-byte loads (thread-major)
+            uint32_t kall[CH == OT ? OT : 1], vall[CH == OT ? OT : 1];
+            if constexpr (CH == OT) {
+                if (!C2_SKIP(32)) {
+                    c2_ld_slots<OT>(rk, tl, kall);
+                    c2_ld_slots<OT>(rv, tl, vall);
+                }
+            }
             cx<float> u0{0.f, 0.f}, u1{0.f, 0.f};
 #pragma unroll
             for (int j0 = 0; j0 < OT; j0 += CH) {
@@ -680,9 +707,14 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
                         wa[i] = make_uint2(8u * (uint32_t)c2pos((int)r), 8u * (uint32_t)c2pos(8192 - (int)r));
                         continue;
                     }
-                    ka[i] = c2_ldu(rk, 4 * tl, 4 * j * C2_T);
+                    if constexpr (CH == OT) {
+                        ka[i] = kall[j];
+                        vv[i] = __uint_as_float(vall[j]);
+                    } else {
+                        ka[i] = c2_ldu(rk, 4 * OTP * tl, 4 * j);
+                        vv[i] = c2_ldf(rv, 4 * OTP * tl, 4 * j);
+                    }
                     gc[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, 16 * tl, 16 * j * C2_T, 0));
-                    vv[i] = c2_ldf(rv, 4 * tl, 4 * j * C2_T);
                     if (!C2_ROWS_DERIVE)
                         wa[i] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rw, 8 * tl, 8 * j * C2_T, 0));
                 }

@@ -74,7 +74,7 @@ struct sg_amp_plan {
     uint32_t *c_kt = nullptr;
     // split per-codeword engine (amp_cw2.hip): outputs per thread (0 = not built) and its tables
     int cw2OT = 0;
-    uint32_t *c2_ka = nullptr, *c2_cmask = nullptr, *c2_cls = nullptr;
+    uint32_t *c2_ka = nullptr, *c2_kat = nullptr, *c2_cmask = nullptr, *c2_cls = nullptr;
     int32_t *c2_oi = nullptr;
     uint32_t *c2_wab = nullptr, *c2_rab = nullptr;
     void *c2_cf = nullptr, *c2_gf = nullptr;
@@ -220,7 +220,7 @@ static int ensure_ws(sg_amp_plan *p, int B, int t_max) {
         }
         if (p->cw2OT) {
             SG_ALLOC(p->ws_c2xp, Bz * 2 * p->cw2OT * CW2_THREADS * 4);
-            SG_ALLOC(p->ws_c2vz, Bz * p->cw2OT * CW2_THREADS * 4);
+            SG_ALLOC(p->ws_c2vz, Bz * cw2_otp(p->cw2OT) * CW2_THREADS * 4);
             SG_ALLOC(p->ws_c2ys, Bz * p->cw2OT * CW2_THREADS * 4);
             SG_ALLOC(p->ws_c2zs, Bz * p->cw2OT * CW2_THREADS * 4);
             SG_ALLOC(p->ws_c2part, Bz * 2 * p->Lblk * 16);
@@ -613,6 +613,13 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
     SG_TRY(upload(p, &p->c2_cls, cls2));
     SG_TRY(upload(p, &p->c2_cmask, cmask));
     SG_TRY(upload(p, &p->c2_ka, ka));
+    {  // thread-major copy: thread tid's slots at [tid][OTP] (amp_cw2.hip loads them 16 bytes at a time)
+        const int OTP = cw2_otp(OT);
+        std::vector<uint32_t> kat((size_t)OTP * T, 0u);
+        for (int tid = 0; tid < T; ++tid)
+            for (int j = 0; j < OT; ++j) kat[(size_t)tid * OTP + j] = ka[(size_t)j * T + tid];
+        SG_TRY(upload(p, &p->c2_kat, kat));
+    }
     SG_TRY(upload(p, &p->c2_oi, oi));
     SG_TRY(upload(p, &p->c2_wab, wab));
     SG_TRY(upload(p, &p->c2_rab, rab));
@@ -907,7 +914,7 @@ static Cw2Tables c2tables(const sg_amp_plan *p, int B) {
     tb.L = p->L; tb.M = p->M; tb.LM = p->LM; tb.n = p->n; tb.N2 = p->N2; tb.Q = p->rQ; tb.Lblk = p->Lblk;
     tb.OT = p->cw2OT; tb.maxcls = p->rmaxcls;
     tb.inv_n2 = 1.0f / (float)p->N2;
-    tb.cmask = p->c2_cmask; tb.ka = p->c2_ka; tb.oi = p->c2_oi;
+    tb.cmask = p->c2_cmask; tb.ka = p->c2_ka; tb.kat = p->c2_kat; tb.oi = p->c2_oi;
     tb.cf = (const float4 *)p->c2_cf; tb.gf = (const float4 *)p->c2_gf;
     tb.cls_ptr = p->r_cls_ptr; tb.cls_ls = p->r_cls_ls; tb.cls2 = p->c2_cls; tb.qpos = p->r_qpos; tb.seg = p->r_seg;
     tb.xr = (float *)p->ws_c2xp; tb.vz = (float *)p->ws_c2vz; tb.ys = (float *)p->ws_c2ys; tb.zs = (float *)p->ws_c2zs; tb.wab = (const uint2 *)p->c2_wab; tb.rab = (const uint2 *)p->c2_rab; tb.part = (float4 *)p->ws_c2part;
