@@ -417,8 +417,9 @@ def amp_decodable(args, d, comm, cpu_seconds, procs):
 
 def amp_f64(args, d, comm, cpu_seconds, procs, steps=2):
     """C2 at the reference's precision: the same design and Philox batch in
-    double precision (the f64 engine: staged regular engine, amp_fused.hip;
-    the reference computes in float64 with a float128 softmax, sparc.py:429-432,
+    double precision (the f64 engines: the split per-codeword engine,
+    amp_cw2d.hip, handing over to the staged regular engine, amp_fused.hip,
+    once half the batch has stopped; the reference computes in float64 with a float128 softmax, sparc.py:429-432,
     463), with its decisions compared codeword by codeword with the CPU
     restatement on a bounded sample."""
     a = argparse.Namespace(**{**vars(args), "precision": "f64"})
@@ -444,7 +445,8 @@ def amp_f64(args, d, comm, cpu_seconds, procs, steps=2):
                        "same design and batch as the f32 line",
            "value": d.world * st["B"] * steps / el, "unit": "codewords/s", "dtype": "f64",
            "batch_per_gpu": st["B"], "steps": steps, "avg_iterations": float(tf.mean()),
-           "engine": {1: "staged (amp_fused.hip)", 0: "general (amp_dct.hip)"}.get(
+           "engine": {2: "split per-codeword (amp_cw2d.hip), staged after the hand-over",
+                      1: "staged (amp_fused.hip)", 0: "general (amp_dct.hip)"}.get(
                _native.lib().sg_amp_plan_engine(st["plan"], st["B"]), "?"),
            "section_errors": int(cnt[0]), "bit_errors": int(cnt[1]), "codeword_errors": int(cnt[2]),
            "roofline": {"bound": "valu-f64", "achieved": tfl, "peak": VALU_F64_PEAK_TFS, "unit": "TFLOP/s",

@@ -235,6 +235,28 @@ struct Cw2Tables {
 };
 int cw2_launch_iter(const Cw2Tables &tb, const RegBufs<float> &bf, const AmpScalars &sc, const AmpParams &pr, int t,
                     hipStream_t s);
+// The same engine in double precision (amp_cw2d.hip): the split engine's slot and class tables, double
+// coefficients, the slots' w_N2^a (Horner / rotation steps over the classes) and the P-point stage twiddles.
+// One 512-thread workgroup per CU (the complex double image is 132 KB).
+struct Cw2dTables {
+    int L, M, LM, n, N2, Q, Lblk, OT, maxcls;
+    const uint32_t *cmask, *ka, *kat;  // as Cw2Tables
+    const int32_t *oi;
+    const double *cf;         // [OT][512][4] (c1, c2): output = Re(c1 H[a] + c2 conj H[N2 - a])
+    const double *gf;         // [OT][512][4] (al, be): G[a] += al z/phi, G[N2 - a] += be z/phi
+    const double *sat;        // [512][OTP][2] w_N2^a of the slot, thread-major (invalid / padding slots: 1)
+    const double *twp;        // [8192][2] w_8192^k
+    const int32_t *cls_ptr;
+    const uint32_t *cls2;
+    const int32_t *qpos;
+    const uint16_t *seg;
+    double *xr;               // [B][2][OT][512] each half's part of the forward output
+    double *vz;               // [B][512][OTP] z / phi, thread-major
+    double *ys, *zs;          // [B][OT][512]
+    double *part;             // [B][2][Lblk][4] (max, sum e, sum e^2, s of the true entry or NaN)
+};
+int cw2d_launch_iter(const Cw2dTables &tb, const RegBufs<double> &bf, const AmpScalars &sc, const AmpParams &pr,
+                     int t, hipStream_t s);
 int cw_launch_iter(const CwTables &tb, const RegBufs<float> &bf, const AmpScalars &sc, const AmpParams &pr, int t,
                    hipStream_t s);
 

@@ -78,6 +78,8 @@ struct sg_amp_plan {
     int32_t *c2_oi = nullptr;
     uint32_t *c2_wab = nullptr, *c2_rab = nullptr;
     void *c2_cf = nullptr, *c2_gf = nullptr;
+    // its double-precision form (amp_cw2d.hip): coefficients, the slots' w_N2^a, the P-point twiddles
+    double *c2d_cf = nullptr, *c2d_gf = nullptr, *c2d_sat = nullptr, *c2d_twp = nullptr;
     void *ws_c2xp = nullptr, *ws_c2vz = nullptr, *ws_c2part = nullptr, *ws_c2ys = nullptr, *ws_c2zs = nullptr;
     uint16_t *c_cmask = nullptr;  // [Q + 1][1024] per-codeword engine: written image values per thread
     int32_t *c_oa = nullptr, *c_ob = nullptr, *c_gi = nullptr;
@@ -218,12 +220,12 @@ static int ensure_ws(sg_amp_plan *p, int B, int t_max) {
             SG_ALLOC(p->tprof, p->tprof_items * 20 * sizeof(uint64_t));
             SG_HIP(hipMemset(p->tprof, 0, p->tprof_items * 20 * sizeof(uint64_t)));
         }
-        if (p->cw2OT) {
-            SG_ALLOC(p->ws_c2xp, Bz * 2 * p->cw2OT * CW2_THREADS * 4);
-            SG_ALLOC(p->ws_c2vz, Bz * cw2_otp(p->cw2OT) * CW2_THREADS * 4);
-            SG_ALLOC(p->ws_c2ys, Bz * p->cw2OT * CW2_THREADS * 4);
-            SG_ALLOC(p->ws_c2zs, Bz * p->cw2OT * CW2_THREADS * 4);
-            SG_ALLOC(p->ws_c2part, Bz * 2 * p->Lblk * 16);
+        if (p->cw2OT) {  // (reals of the plan's precision; partial statistics: four per section)
+            SG_ALLOC(p->ws_c2xp, Bz * 2 * p->cw2OT * CW2_THREADS * rs);
+            SG_ALLOC(p->ws_c2vz, Bz * cw2_otp(p->cw2OT) * CW2_THREADS * rs);
+            SG_ALLOC(p->ws_c2ys, Bz * p->cw2OT * CW2_THREADS * rs);
+            SG_ALLOC(p->ws_c2zs, Bz * p->cw2OT * CW2_THREADS * rs);
+            SG_ALLOC(p->ws_c2part, Bz * 2 * p->Lblk * 4 * rs);
         }
         SG_ALLOC(p->ws_stM, Bz * p->L * rs);
         SG_ALLOC(p->ws_stI, Bz * p->L * rs);
@@ -552,6 +554,11 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
     std::vector<uint32_t> ka((size_t)OT * T, 0u);
     std::vector<int32_t> oi((size_t)OT * T, 0);
     std::vector<float> cf((size_t)OT * T * 4, 0.f), gf((size_t)OT * T * 4, 0.f);
+    const bool f64 = p->precision == SG_F64;
+    const int OTP = cw2_otp(OT);
+    std::vector<double> cfd(f64 ? (size_t)OT * T * 4 : 0, 0.0), gfd(f64 ? (size_t)OT * T * 4 : 0, 0.0),
+        sat(f64 ? (size_t)OTP * T * 2 : 0, 0.0);
+    for (size_t i = 0; i < sat.size(); i += 2) sat[i] = 1.0;  // invalid and padding slots: S = 1
     std::vector<uint32_t> wab((size_t)OT * T * 2, 4u * CW2_TRASH), rab((size_t)OT * T * 2, 0u);
     for (int tid = 0; tid < T; ++tid) {
         int j = 0;
@@ -577,6 +584,15 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
                                     (float)o.al.real(), (float)o.al.imag(), (float)o.be.real(), (float)o.be.imag()};
                 std::copy(v, v + 4, cf.begin() + 4 * c);
                 std::copy(v + 4, v + 8, gf.begin() + 4 * c);
+                if (f64) {
+                    const double d[8] = {o.c1.real(), o.c1.imag(), o.c2.real(), o.c2.imag(),
+                                         o.al.real(), o.al.imag(), o.be.real(), o.be.imag()};
+                    std::copy(d, d + 4, cfd.begin() + 4 * c);
+                    std::copy(d + 4, d + 8, gfd.begin() + 4 * c);
+                    const cd w = tw(o.a, N2);  // S = w_N2^a (amp_cw2d.hip: Horner / rotation step per class)
+                    sat[((size_t)tid * OTP + j) * 2] = w.real();
+                    sat[((size_t)tid * OTP + j) * 2 + 1] = w.imag();
+                }
             }
         }
     }
@@ -628,6 +644,18 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
     SG_TRY(upload(p, &dgf, gf));
     p->c2_cf = dcf;
     p->c2_gf = dgf;
+    if (f64) {
+        std::vector<double> twp((size_t)P * 2);
+        for (int k = 0; k < P; ++k) {
+            const cd w = tw(k, P);
+            twp[2 * k] = w.real();
+            twp[2 * k + 1] = w.imag();
+        }
+        SG_TRY(upload(p, &p->c2d_cf, cfd));
+        SG_TRY(upload(p, &p->c2d_gf, gfd));
+        SG_TRY(upload(p, &p->c2d_sat, sat));
+        SG_TRY(upload(p, &p->c2d_twp, twp));
+    }
     p->cw2OT = OT;
     return SG_OK;
 }
@@ -867,6 +895,13 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
         SG_TRY(build_cw(p, row_k1[0], kptr[0], kk2[0], f_oa, f_ob, f_gi, f_gc, cls_ptr, cls_ls));
         if (p->cw) SG_TRY(build_cw2(p, order0, t_scale[0], row_k1[0], cls_ptr, cls_ls));
     }
+    // double precision: the split engine only (amp_cw2d.hip), its tables built directly; the plan then
+    // counts as a per-codeword plan (use_cw), without the companion (f64 keeps P = 8192 either way)
+    if (p->precision == SG_F64 && nT == 1 && P == (1 << 13) && Lblk <= 2 * CW2_THREADS && p->L <= 1024 &&
+        Q % 2 == 0 && Q <= 70 && p->rmaxcls <= CW2_SLICE && !p->no_cw) {
+        SG_TRY(build_cw2(p, order0, t_scale[0], row_k1[0], cls_ptr, cls_ls));
+        p->cw = p->cw2OT != 0;
+    }
     return SG_OK;
 }
 
@@ -927,6 +962,18 @@ static Cw2Tables c2tables(const sg_amp_plan *p, int B) {
 // The split engine (amp_cw2.hip) runs the per-codeword engine's iterations
 // when its tables were built; SG_AMP_CW2=0 keeps the one-workgroup form
 // (A/B tests).
+static Cw2dTables c2dtables(const sg_amp_plan *p) {
+    Cw2dTables tb;
+    tb.L = p->L; tb.M = p->M; tb.LM = p->LM; tb.n = p->n; tb.N2 = p->N2; tb.Q = p->rQ; tb.Lblk = p->Lblk;
+    tb.OT = p->cw2OT; tb.maxcls = p->rmaxcls;
+    tb.cmask = p->c2_cmask; tb.ka = p->c2_ka; tb.kat = p->c2_kat; tb.oi = p->c2_oi;
+    tb.cf = p->c2d_cf; tb.gf = p->c2d_gf; tb.sat = p->c2d_sat; tb.twp = p->c2d_twp;
+    tb.cls_ptr = p->r_cls_ptr; tb.cls2 = p->c2_cls; tb.qpos = p->r_qpos; tb.seg = p->r_seg;
+    tb.xr = (double *)p->ws_c2xp; tb.vz = (double *)p->ws_c2vz; tb.ys = (double *)p->ws_c2ys;
+    tb.zs = (double *)p->ws_c2zs; tb.part = (double *)p->ws_c2part;
+    return tb;
+}
+
 static bool use_cw2(const sg_amp_plan *p) {
     if (!p->cw2OT) return false;
     const char *e = std::getenv("SG_AMP_CW2");
@@ -1397,7 +1444,8 @@ static int decode_regular(sg_amp_plan *p, const void *d_y, int B, const int32_t 
     pr.phi_method = phi_method; pr.t_max = t_max;
     SG_TRY(reg_launch_init(B, p->Lc, t_max, p->ws_nmse, p->ws_active, p->ws_tfinal, s));
     ActivePoll poll{p, B, s};
-    bool cw =std::is_same<T, float>::value && use_cw(p, B);
+    // (double precision has the split engine only: SG_AMP_CW2=0 leaves it the staged engine)
+    bool cw = use_cw(p, B) && (std::is_same<T, float>::value || use_cw2(p));
     p->last_engine = cw ? 2 : 1;
     p->last_handover = -1;
     const char *eng = std::getenv("SG_AMP_ENGINE");
@@ -1411,6 +1459,8 @@ static int decode_regular(sg_amp_plan *p, const void *d_y, int B, const int32_t 
                 if (use_cw2(p)) SG_TRY(cw2_launch_iter(c2tables(p, B), bf, sc, pr, t, s));
                 else SG_TRY(cw_launch_iter(ctables(p, B), bf, sc, pr, t, s));
             }
+        } else {
+            if (cw) SG_TRY(cw2d_launch_iter(c2dtables(p), bf, sc, pr, t, s));
         }
         if (!cw) {
             if (t > 0) SG_TRY(reg_launch_ab<T>(tb, bf, s));
@@ -1609,7 +1659,7 @@ int sg_amp_plan_create(int ndim, const double *W, int Lr, int Lc, int L, int M, 
                        const uint32_t *order1, int precision, sg_amp_plan **out) {
     sg_amp_plan *p = nullptr;
     SG_TRY(build_plan(ndim, W, Lr, Lc, L, M, n, order0, order1, precision, false, &p));
-    if (p->cw) {
+    if (p->cw && precision == SG_F32) {
         const int rc = build_plan(ndim, W, Lr, Lc, L, M, n, order0, order1, precision, true, &p->alt);
         if (rc != SG_OK) {
             sg_amp_plan_destroy(p);
@@ -1637,7 +1687,7 @@ int sg_amp_plan_destroy(sg_amp_plan *p) {
 
 int sg_amp_plan_engine(const sg_amp_plan *p, int B) {
     SG_CHECK_ARG(p, "plan is NULL");
-    if (p->regular) return (p->precision == SG_F32 && sg::use_cw(p, B)) ? 2 : 1;
+    if (p->regular) return (sg::use_cw(p, B) && (p->precision == SG_F32 || sg::use_cw2(p))) ? 2 : 1;
     return (p->block || p->block2) ? 3 : 0;
 }
 
