@@ -244,14 +244,14 @@ struct Cw2dTables {
     const int32_t *oi;
     const double *cf;         // [OT][512][4] (c1, c2): output = Re(c1 H[a] + c2 conj H[N2 - a])
     const double *gf;         // [OT][512][4] (al, be): G[a] += al z/phi, G[N2 - a] += be z/phi
-    const double *sat;        // [512][OTP][2] w_N2^a of the slot, thread-major (invalid / padding slots: 1)
+    const double *sa;         // [OT][512][2] w_N2^a of the slot (invalid slots: 1)
     const double *twp;        // [8192][2] w_8192^k
     const int32_t *cls_ptr;
     const uint32_t *cls2;
     const int32_t *qpos;
     const uint16_t *seg;
     double *xr;               // [B][2][OT][512] each half's part of the forward output
-    double *vz;               // [B][512][OTP] z / phi, thread-major
+    double *vz;               // [B][OT][512] z / phi
     double *ys, *zs;          // [B][OT][512]
     double *part;             // [B][2][Lblk][4] (max, sum e, sum e^2, s of the true entry or NaN)
 };

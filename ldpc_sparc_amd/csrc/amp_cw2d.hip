@@ -45,6 +45,14 @@ namespace sg {
 namespace {
 
 constexpr int D_T = CW2_THREADS;  // 512
+// Phase ablation for timing studies only (tools/mk_variant.sh ... -DD_ABL=<mask>; results are garbage, the
+// shipped build has 0): Ab 1 FFT, 2 accumulation, 4 slice loads, 8 beta exponentials, 16 beta stores,
+// 32 scatter; Az 64 FFT, 128 rows, 256 slice loads, 512 statistics, 1024 s stores, 2048 statistics'
+// exponentials
+#ifndef D_ABL
+#define D_ABL 0
+#endif
+#define D_SKIP(bit) ((D_ABL & (bit)) != 0)
 constexpr int D_P = 8192;
 constexpr int D_SC = 9, D_NC = 2, D_SN = D_SC * D_NC;  // 18 class entries per thread (CW2_SLICE / 512)
 static_assert(D_SN * D_T == CW2_SLICE, "class slices of 18 entries per thread");
@@ -297,6 +305,18 @@ __device__ __forceinline__ void d_ld_slots(__amdgpu_buffer_rsrc_t r, int tl, uin
     }
 }
 
+// x when i < n, else the double whose high word is fill (low word 0), by bit masks: written as a compare
+// and a select, the 16 entries' lane masks stayed live in SGPR pairs across the exponentials, were
+// spilled to VGPR lanes, and the results moved in the ninth digit (tools/f64_diff.py)
+__device__ __forceinline__ double d_keep(double x, int i, int n, uint32_t fill) {
+    typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+    const uint32_t mk = (uint32_t)((i - n) >> 31);  // all ones inside
+    u2 u = __builtin_bit_cast(u2, x);
+    u[0] &= mk;
+    u[1] = (u[1] & mk) | (fill & ~mk);
+    return __builtin_bit_cast(double, u);
+}
+
 // S^e for a uniform exponent e (square and multiply)
 __device__ __forceinline__ d2 d_pow(d2 s, int e) {
     d2 w = d2{1.0, 0.0};
@@ -333,14 +353,16 @@ __global__ __launch_bounds__(D_T, 1) void cw2d_ab(Cw2dTables tb, RegBufs<double>
     d_tw1_init<false>(tid, tb.twp);
     const int *cpl = d_stage_cp(smem, tb, tid);
     __syncthreads();
-    constexpr int OTP = cw2_otp(OT);
-    const __amdgpu_buffer_rsrc_t rk = d_rsrc(tb.kat, 4 * OTP * D_T), rS = d_rsrc(tb.sat, 16 * OTP * D_T);
+    const __amdgpu_buffer_rsrc_t rk = d_rsrc(tb.ka, 4 * OT * D_T), rS = d_rsrc(tb.sa, 16 * OT * D_T);
     // the thread's slot words and S = w_N2^a (reloaded per class from L1 / L2: held across the
-    // transform beside H they spill)
+    // transform beside H they spill), slot-major: every load a contiguous run of the wavefront's lanes
+    // (thread-major rows of 12 complex doubles put each lane on its own cache lines: profiles/r05_f64_ablation.txt)
     auto acc_tables = [&](int tl, uint32_t *ka, d2 *S) {
-        d_ld_slots<OT>(rk, tl, ka);
 #pragma unroll
-        for (int j = 0; j < OT; ++j) S[j] = d_ld2(rS, 16 * OTP * tl, 16 * j);
+        for (int j = 0; j < OT; ++j) {
+            ka[j] = __builtin_amdgcn_raw_buffer_load_b32(rk, 4 * tl, 4 * j * D_T, 0);
+            S[j] = d_ld2(rS, 16 * tl, 16 * j * D_T);
+        }
     };
     // Horner step of class m's transform (still in the image) for every owned output
     // (four slots' image reads at a time: all of them in flight beside H, S and the next class's slice
@@ -372,24 +394,29 @@ __global__ __launch_bounds__(D_T, 1) void cw2d_ab(Cw2dTables tb, RegBufs<double>
             const __amdgpu_buffer_rsrc_t re = d_rsrc(tb.cls2 + (size_t)m2 * CW2_SLICE, 4 * CW2_SLICE);
 #pragma unroll
             for (int i = 0; i < D_SN; ++i) {
+                if (D_SKIP(4)) {  // (synthetic entries inside the image, section 0)
+                    v[i] = (double)(tl + i);
+                    e[i] = (uint32_t)(((tl * 37 + i * 4099) & 8191) * 2);
+                    continue;
+                }
                 v[i] = d_ldd(rs, 8 * tl + 8 * i * D_T, 0);
                 e[i] = __builtin_amdgcn_raw_buffer_load_b32(re, 4 * tl, 4 * i * D_T, 0);
             }
         }
         const uint32_t cmk = tb.cmask[m2 * D_T + tl];
-        if (prev) {
+        if (prev && !D_SKIP(2)) {
             accumulate(ka, S);
             __syncthreads();  // the image is read before the scatter overwrites it
         }
 #pragma unroll
         for (int i = 0; i < D_SN; ++i) {  // beta = eta(s), sparc.py:429-432 (padded entries: the trash slot)
             const d2 mi = *d_at(D_STAT + (int)(e[i] >> 16));
-            const double b = exp(d_arg(v[i], mi.x, tau, inv_tau)) * mi.y;
-            *d_re(e[i] & 0xffffu) = b;
-            d_std(rs, b, 8 * tl + 8 * i * D_T, 0);
+            const double b = (D_SKIP(8) ? v[i] : exp(d_arg(v[i], mi.x, tau, inv_tau))) * mi.y;
+            if (!D_SKIP(32)) *d_re(e[i] & 0xffffu) = b;
+            if (!D_SKIP(16)) d_std(rs, b, 8 * tl + 8 * i * D_T, 0);
         }
         __syncthreads();
-        d_fft<false>(tl, cmk, tb.twp);
+        if (!D_SKIP(1)) d_fft<false>(tl, cmk, tb.twp);
     }
     {
         uint32_t ka[OT];
@@ -404,7 +431,7 @@ __global__ __launch_bounds__(D_T, 1) void cw2d_ab(Cw2dTables tb, RegBufs<double>
     for (int j = 0; j < OT; ++j) {
         d2 ha = Ha[j], hb = Hb[j];
         if (mlo > 0) {
-            const d2 w0 = d_pow(d_ld2(rS, 16 * OTP * tid, 16 * j), mlo);
+            const d2 w0 = d_pow(d_ld2(rS, 16 * tid, 16 * j * D_T), mlo);
             ha = dmul(ha, w0);
             hb = dmul(hb, w0);
         }
@@ -506,13 +533,9 @@ __global__ __launch_bounds__(D_T) void cw2d_ctrl(Cw2dTables tb, RegBufs<double> 
         bf.phi[cw] = phi;
         bf.tau[cw] = tv_new;
     }
-    constexpr int OTP = cw2_otp(OT);
-    d2 *vz2 = reinterpret_cast<d2 *>(tb.vz + ((size_t)cw * D_T + tid) * OTP);  // thread-major
+    double *vz = tb.vz + (size_t)cw * OT * D_T;  // slot-major
 #pragma unroll
-    for (int q = 0; q < OTP / 2; ++q) {  // z / phi (sparc.py:972); padding slots 0
-        const double a = 2 * q < OT ? zr[2 * q] / phi : 0.0, b = 2 * q + 1 < OT ? zr[2 * q + 1] / phi : 0.0;
-        vz2[q] = d2{a, b};
-    }
+    for (int j = 0; j < OT; ++j) vz[j * D_T + tid] = zr[j] / phi;  // z / phi (sparc.py:972)
 }
 
 // ---------------------------------------------------------------------------- Az
@@ -525,8 +548,7 @@ __global__ __launch_bounds__(D_T, 1) void cw2d_az(Cw2dTables tb, RegBufs<double>
     const bool have_beta = t > 0;
     const double tau = bf.tau[cw], inv_tau = 1.0 / tau;
     double *s = bf.s + (size_t)cw * tb.LM;
-    constexpr int OTP = cw2_otp(OT);
-    const double *vz = tb.vz + (size_t)cw * OTP * D_T;
+    const double *vz = tb.vz + (size_t)cw * OT * D_T;
     const int Lb = tb.Lblk;
     const int Qh = tb.Q >> 1, mlo = h * Qh, mhi = mlo + Qh;
     // running statistics of sections tid and tid + 512 over this half's classes
@@ -537,35 +559,32 @@ __global__ __launch_bounds__(D_T, 1) void cw2d_az(Cw2dTables tb, RegBufs<double>
         const int sec = tid + k * D_T;
         if (bf.true_idx && sec < Lb) jt[k] = tb.qpos[sec * tb.M + bf.true_idx[lb + sec]];
     }
-    const __amdgpu_buffer_rsrc_t rS = d_rsrc(tb.sat, 16 * OTP * D_T);
+    const __amdgpu_buffer_rsrc_t rS = d_rsrc(tb.sa, 16 * OT * D_T);
     d2 W[OT];  // w_N2^(m a) of the class, rotated by S = w_N2^a per class (S reloaded per class)
 #pragma unroll
-    for (int j = 0; j < OT; ++j) W[j] = d_pow(d_ld2(rS, 16 * OTP * tid, 16 * j), mlo);
+    for (int j = 0; j < OT; ++j) W[j] = d_pow(d_ld2(rS, 16 * tid, 16 * j * D_T), mlo);
     d_tw1_init<true>(tid, tb.twp);
     const int *cpl = d_stage_cp(smem, tb, tid);
     __syncthreads();
-    const __amdgpu_buffer_rsrc_t rv = d_rsrc(vz, 8 * OTP * D_T), rk = d_rsrc(tb.kat, 4 * OTP * D_T),
+    const __amdgpu_buffer_rsrc_t rv = d_rsrc(vz, 8 * OT * D_T), rk = d_rsrc(tb.ka, 4 * OT * D_T),
                                  rg = d_rsrc(tb.gf, 32 * OT * D_T);
     for (int m2 = mlo; m2 < mhi; ++m2) {
         const int tl = d_opaque(tid);
         const uint32_t rmk = tb.cmask[tb.Q * D_T + tl];
         const int q0 = d_uni(cpl[m2]), q1 = d_uni(cpl[m2 + 1]);
         const __amdgpu_buffer_rsrc_t rs = d_rsrc(s + q0, 8 * (q1 - q0));
-        {
+        if (!D_SKIP(128)) {
             // rows r and P - r of each owned pair: sums of al v conj(W) / be v W over its outputs (v = z / phi),
             // branch-free as amp_cw2.hip's rows (NEWROW restarts the sums; both rows written on the pair's last
             // slot, the trash slot otherwise; r = 0, P / 2: the sum at row r)
             uint32_t kall[OT];
-            double vall[OTP];
+            double vall[OT];
             d2 S[OT];
-            d_ld_slots<OT>(rk, tl, kall);
 #pragma unroll
-            for (int j = 0; j < OT; ++j) S[j] = d_ld2(rS, 16 * OTP * tl, 16 * j);
-#pragma unroll
-            for (int q = 0; q < OTP / 2; ++q) {
-                const d2 p = d_ld2(rv, 8 * OTP * tl, 16 * q);
-                vall[2 * q] = p.x;
-                vall[2 * q + 1] = p.y;
+            for (int j = 0; j < OT; ++j) {  // (slot-major: contiguous per wavefront, see cw2d_ab)
+                kall[j] = __builtin_amdgcn_raw_buffer_load_b32(rk, 4 * tl, 4 * j * D_T, 0);
+                vall[j] = d_ldd(rv, 8 * tl, 8 * j * D_T);
+                S[j] = d_ld2(rS, 16 * tl, 16 * j * D_T);
             }
             constexpr int CH = 4;  // slots per round of coefficient loads
             d2 u0{0.0, 0.0}, u1{0.0, 0.0};
@@ -603,6 +622,11 @@ __global__ __launch_bounds__(D_T, 1) void cw2d_az(Cw2dTables tb, RegBufs<double>
             const __amdgpu_buffer_rsrc_t re = d_rsrc(tb.cls2 + (size_t)m2 * CW2_SLICE, 4 * CW2_SLICE);
 #pragma unroll
             for (int i = 0; i < D_SN; ++i) {
+                if (D_SKIP(256)) {
+                    v[i] = (double)(tl + i);
+                    e[i] = (uint32_t)(((tl * 37 + i * 4099) & 8191) * 2);
+                    continue;
+                }
                 e[i] = __builtin_amdgcn_raw_buffer_load_b32(re, 4 * tl, 4 * i * D_T, 0);
                 v[i] = d_ldd(rs, 8 * tl + 8 * i * D_T, 0);  // (t = 0: unused)
             }
@@ -618,7 +642,7 @@ __global__ __launch_bounds__(D_T, 1) void cw2d_az(Cw2dTables tb, RegBufs<double>
             }
         }
         __syncthreads();
-        d_fft<true>(tl, rmk, tb.twp);
+        if (!D_SKIP(64)) d_fft<true>(tl, rmk, tb.twp);
         double snv[D_SN];
 #pragma unroll
         for (int i = 0; i < D_SN; ++i) {  // s = beta_prev + tau u (sparc.py:972); beta_prev stored by cw2d_ab
@@ -626,7 +650,8 @@ __global__ __launch_bounds__(D_T, 1) void cw2d_az(Cw2dTables tb, RegBufs<double>
             snv[i] = b + tau * *d_re(e[i] & 0xffffu);
         }
 #pragma unroll
-        for (int c = 0; c < D_SN; ++c) d_std(rs, snv[c], 8 * tl + 8 * c * D_T, 0);  // s to HBM (class order)
+        for (int c = 0; c < D_SN; ++c)  // s to HBM (class order)
+            if (!D_SKIP(1024)) d_std(rs, snv[c], 8 * tl + 8 * c * D_T, 0);
         __syncthreads();
 #pragma unroll
         for (int c = 0; c < D_SN; ++c) *d_re(tl + c * D_T) = snv[c];  // s of the class in class order
@@ -635,12 +660,20 @@ __global__ __launch_bounds__(D_T, 1) void cw2d_az(Cw2dTables tb, RegBufs<double>
         // (1) each section's segment maximum, one thread per section; (2) e = exp(s / tau - max / tau)
         // of the thread's own entries (one exponential per entry, not one per entry of the longest
         // segment of the wavefront); (3) the segment sums of e and e^2, merged into the running statistics
+        // (segments average LM / (Q L) = 8 entries: the first 16 are read unconditionally -- inside the
+        // image past the segment too -- and masked, one LDS round trip; longer ones loop)
+        constexpr int RC = 16;
         double msg[2];
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < (D_SKIP(512) ? 0 : 2); ++k) {
             const int a = sa[k], n = sb[k] - sa[k];
-            double m = -INFINITY;
-            for (int i = 0; i < n; ++i) m = fmax(m, *d_re(a + i));
+            double x[RC];
+#pragma unroll
+            for (int i = 0; i < RC; ++i) x[i] = d_keep(*d_re(a + i), i, n, 0xfff00000u);  // past the end: -inf
+            double m = x[0];
+#pragma unroll
+            for (int i = 1; i < RC; ++i) m = fmax(m, x[i]);
+            for (int c = RC; c < n; ++c) m = fmax(m, *d_re(a + c));
             msg[k] = m;
             const int sec = tl + k * D_T;
             if (n > 0) *d_re(D_SEGMAX + sec) = m / tau;  // (amp_fused.hip sm_stage)
@@ -649,28 +682,40 @@ __global__ __launch_bounds__(D_T, 1) void cw2d_az(Cw2dTables tb, RegBufs<double>
         __syncthreads();
 #pragma unroll
         for (int c = 0; c < D_SN; ++c) {  // (padded entries: section 0, their values unread)
+            if (D_SKIP(512)) break;
             const double ms = *d_re(D_SEGMAX + (e[c] >> 16));
-            *d_re(tl + c * D_T) = exp(d_arg(snv[c], ms, tau, inv_tau));
+            *d_re(tl + c * D_T) = D_SKIP(2048) ? snv[c] - ms : exp(d_arg(snv[c], ms, tau, inv_tau));
         }
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < (D_SKIP(512) ? 0 : 2); ++k) {
             const int a = sa[k], n = sb[k] - sa[k];
             if (n <= 0) continue;
             double S1 = 0.0, S2 = 0.0;
-            for (int i = 0; i < n; ++i) {
-                const double x = *d_re(a + i);
-                S1 += x;
-                S2 += x * x;
+            double x[RC];
+#pragma unroll
+            for (int i = 0; i < RC; ++i) x[i] = d_keep(*d_re(a + i), i, n, 0u);  // past the end: 0
+#pragma unroll
+            for (int i = 0; i < RC; ++i) {
+                S1 += x[i];
+                S2 = __builtin_fma(x[i], x[i], S2);
+            }
+            for (int c = RC; c < n; ++c) {
+                const double e1 = *d_re(a + c);
+                S1 += e1;
+                S2 = __builtin_fma(e1, e1, S2);
             }
             const double m = msg[k];
-            if (m > Mr[k]) {  // the staged merge's factor exp(m_c / tau - M / tau) (amp_fused.hip sm_arg)
-                const double f = exp(Mr[k] / tau - m / tau);
+            // the staged merge's factor exp(m_c / tau - M / tau) (amp_fused.hip sm_arg), both quotients by
+            // the Markstein division (an empty running maximum: factor 0)
+            const double qm = d_arg(m, 0.0, tau, inv_tau), qr = d_arg(Mr[k], 0.0, tau, inv_tau);
+            if (m > Mr[k]) {
+                const double f = Mr[k] == -INFINITY ? 0.0 : exp(qr - qm);
                 R1[k] = R1[k] * f + S1;
                 R2[k] = R2[k] * (f * f) + S2;
                 Mr[k] = m;
             } else {
-                const double f = exp(m / tau - Mr[k] / tau);
+                const double f = exp(qm - qr);
                 R1[k] += S1 * f;
                 R2[k] += S2 * (f * f);
             }

@@ -79,7 +79,7 @@ struct sg_amp_plan {
     uint32_t *c2_wab = nullptr, *c2_rab = nullptr;
     void *c2_cf = nullptr, *c2_gf = nullptr;
     // its double-precision form (amp_cw2d.hip): coefficients, the slots' w_N2^a, the P-point twiddles
-    double *c2d_cf = nullptr, *c2d_gf = nullptr, *c2d_sat = nullptr, *c2d_twp = nullptr;
+    double *c2d_cf = nullptr, *c2d_gf = nullptr, *c2d_sa = nullptr, *c2d_twp = nullptr;
     void *ws_c2xp = nullptr, *ws_c2vz = nullptr, *ws_c2part = nullptr, *ws_c2ys = nullptr, *ws_c2zs = nullptr;
     uint16_t *c_cmask = nullptr;  // [Q + 1][1024] per-codeword engine: written image values per thread
     int32_t *c_oa = nullptr, *c_ob = nullptr, *c_gi = nullptr;
@@ -555,10 +555,9 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
     std::vector<int32_t> oi((size_t)OT * T, 0);
     std::vector<float> cf((size_t)OT * T * 4, 0.f), gf((size_t)OT * T * 4, 0.f);
     const bool f64 = p->precision == SG_F64;
-    const int OTP = cw2_otp(OT);
     std::vector<double> cfd(f64 ? (size_t)OT * T * 4 : 0, 0.0), gfd(f64 ? (size_t)OT * T * 4 : 0, 0.0),
-        sat(f64 ? (size_t)OTP * T * 2 : 0, 0.0);
-    for (size_t i = 0; i < sat.size(); i += 2) sat[i] = 1.0;  // invalid and padding slots: S = 1
+        sad(f64 ? (size_t)OT * T * 2 : 0, 0.0);
+    for (size_t i = 0; i < sad.size(); i += 2) sad[i] = 1.0;  // invalid slots: S = 1
     std::vector<uint32_t> wab((size_t)OT * T * 2, 4u * CW2_TRASH), rab((size_t)OT * T * 2, 0u);
     for (int tid = 0; tid < T; ++tid) {
         int j = 0;
@@ -590,8 +589,8 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
                     std::copy(d, d + 4, cfd.begin() + 4 * c);
                     std::copy(d + 4, d + 8, gfd.begin() + 4 * c);
                     const cd w = tw(o.a, N2);  // S = w_N2^a (amp_cw2d.hip: Horner / rotation step per class)
-                    sat[((size_t)tid * OTP + j) * 2] = w.real();
-                    sat[((size_t)tid * OTP + j) * 2 + 1] = w.imag();
+                    sad[2 * c] = w.real();
+                    sad[2 * c + 1] = w.imag();
                 }
             }
         }
@@ -653,7 +652,7 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
         }
         SG_TRY(upload(p, &p->c2d_cf, cfd));
         SG_TRY(upload(p, &p->c2d_gf, gfd));
-        SG_TRY(upload(p, &p->c2d_sat, sat));
+        SG_TRY(upload(p, &p->c2d_sa, sad));
         SG_TRY(upload(p, &p->c2d_twp, twp));
     }
     p->cw2OT = OT;
@@ -967,7 +966,7 @@ static Cw2dTables c2dtables(const sg_amp_plan *p) {
     tb.L = p->L; tb.M = p->M; tb.LM = p->LM; tb.n = p->n; tb.N2 = p->N2; tb.Q = p->rQ; tb.Lblk = p->Lblk;
     tb.OT = p->cw2OT; tb.maxcls = p->rmaxcls;
     tb.cmask = p->c2_cmask; tb.ka = p->c2_ka; tb.kat = p->c2_kat; tb.oi = p->c2_oi;
-    tb.cf = p->c2d_cf; tb.gf = p->c2d_gf; tb.sat = p->c2d_sat; tb.twp = p->c2d_twp;
+    tb.cf = p->c2d_cf; tb.gf = p->c2d_gf; tb.sa = p->c2d_sa; tb.twp = p->c2d_twp;
     tb.cls_ptr = p->r_cls_ptr; tb.cls2 = p->c2_cls; tb.qpos = p->r_qpos; tb.seg = p->r_seg;
     tb.xr = (double *)p->ws_c2xp; tb.vz = (double *)p->ws_c2vz; tb.ys = (double *)p->ws_c2ys;
     tb.zs = (double *)p->ws_c2zs; tb.part = (double *)p->ws_c2part;

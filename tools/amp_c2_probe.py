@@ -11,21 +11,22 @@ from ldpc_sparc_amd import _native, sparc  # noqa: E402
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 R = float(sys.argv[3]) if len(sys.argv) > 3 else 1.5
+PREC = _native.SG_F64 if len(sys.argv) > 4 and sys.argv[4] == "f64" else _native.SG_F32
 L, M = 1024, 512
 n = int(round(L * 9 / R))
 W = np.array(15.0)
 t0 = time.time()
 o0, o1 = sparc.generate_ordering(W, n, L * M, 0)
 op = sparc.DesignOperator(W, L, M, n, o0, o1)
-plan = op.plan(_native.SG_F32)
+plan = op.plan(PREC)
 print("plan", time.time() - t0, flush=True)
 rng = np.random.default_rng(1)
 true = rng.integers(0, M, (B, L)).astype(np.int32)
 beta0 = np.zeros((B, L * M))
 beta0[np.arange(B)[:, None], np.arange(L) * M + true] = 1
-Y = op.apply(beta0, False, _native.SG_F32) + rng.standard_normal((B, n))
+Y = op.apply(beta0, False, PREC) + rng.standard_normal((B, n))
 lib = _native.lib()
-d_y = _native.DeviceBuffer.from_array(Y.astype(np.float32))
+d_y = _native.DeviceBuffer.from_array(Y.astype(np.float64 if PREC == _native.SG_F64 else np.float32))
 d_true = _native.DeviceBuffer.from_array(true)
 d_map = _native.DeviceBuffer(B * L * 4)
 d_tf = _native.DeviceBuffer(B * 4)
