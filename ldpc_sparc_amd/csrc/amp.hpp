@@ -253,7 +253,8 @@ struct Cw2dTables {
     double *xr;               // [B][2][OT][512] each half's part of the forward output
     double *vz;               // [B][OT][512] z / phi
     double *ys, *zs;          // [B][OT][512]
-    double *part;             // [B][2][Lblk][4] (max, sum e, sum e^2, s of the true entry or NaN)
+    double *beta;             // [B][LM] beta in class order (cw2d_stats -> the next Ab, Az's beta_prev)
+    double *sec;              // [B][L][2] per section: sum beta^2, squared error (cw2d_stats -> cw2d_final)
 };
 int cw2d_launch_iter(const Cw2dTables &tb, const RegBufs<double> &bf, const AmpScalars &sc, const AmpParams &pr,
                      int t, hipStream_t s);

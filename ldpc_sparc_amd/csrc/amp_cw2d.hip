@@ -1,13 +1,12 @@
 // Split per-codeword AMP engine in double precision (the f64 C2 path, what an
 // unmodified sparc_sim caller runs).  Same iteration as amp_cw2.hip --
 // sparc.py:883-999 with the sub-sampled DCT operators of sub_dct :648-701 --
-// as four launches per iteration over the split engine's host tables
-// (build_cw2: output slots grouped by conjugate row pair, class slices, masks):
+// over the split engine's host tables (build_cw2: output slots grouped by
+// conjugate row pair, class slices, first-stage masks), five launches:
 //
 //   cw2d_ab    (2 B)  half h of the Q classes, in DESCENDING class order: beta
-//              of the class (sparc.py:429-432, the staged f64 engine's
-//              argument) -> LDS scatter, stored over s for cw2d_az -> P-point
-//              FFT -> for every owned output, Horner steps
+//              of the class (cw2d_stats' output, class order) -> LDS scatter
+//              -> P-point FFT -> for every owned output, Horner steps
 //                  H[a]      <- H[a] S + Y_m[r],
 //                  conj H[b] <- conj H[b] S + conj Y_m[P - r],  S = w_N2^a,
 //              so the sum over the half's classes of w_N2^(m a) Y_m needs one
@@ -17,20 +16,24 @@
 //   cw2d_az    (2 B)  half h of the classes, ascending: rows r and P - r of each
 //              owned pair from al z/phi conj(W) and be z/phi W (W = w_N2^(m a)
 //              rotated by S per class) -> inverse FFT -> s = beta_prev + tau u
-//              (sparc.py:972) -> per-section (max, sum e, sum e^2) merged over
-//              the classes (e = exp(s / tau - max / tau), the reference's sums).
-//   cw2d_merge (B)  the halves' statistics -> max, 1/sum, psi, NMSE, early stop
-//              (sparc.py:973-988).
+//              (sparc.py:972) in class order.
+//   cw2d_stats (B L / 4)  one wavefront per section: the softmax of s over the
+//              section (sparc.py:429-432) -> beta (class order), section max and
+//              1/sum, sum beta^2 and squared error (sparc.py:973-981).
+//   cw2d_final (B)  psi, NMSE, early stop (sparc.py:973-988).
 //
 // Why a separate engine: the staged f64 engine (amp_fused.hip) passes the
 // needed rows of both FFT stages through HBM (four passes of ~6.5 MB per
 // codeword-iteration at C2, beside 12 MB of s) and runs each class at one
-// workgroup per CU with nothing overlapping its memory phases.  Here the only
-// per-iteration HBM traffic is s (read twice, written twice: beta over s, then
-// s) and the per-codeword slot vectors.  A complex double image of P = 8192
-// points is 132 KB, so one 512-thread workgroup per CU: LDS holds the image,
-// the previous beta's section statistics (16 KB), a trash slot, the first
-// radix-16 stage's twiddles and the class pointers (159.5 KB of 160 KB).
+// workgroup per CU with nothing overlapping its memory phases.  Here the
+// per-iteration HBM traffic is s and beta (Ab reads beta, Az reads beta and
+// writes s, the statistics read s and write beta: 20 MB per codeword-iteration)
+// and the per-codeword slot vectors.  A complex double image of P = 8192 points
+// is 132 KB, so one 512-thread workgroup per CU (8 wavefronts): the softmax and
+// its statistics, whose section reductions need barriers and LDS round trips,
+// run in their own launch at full occupancy instead (inside Az they took half
+// of its time, profiles/r05_f64_ablation.txt), and the exponentials are one per
+// entry and iteration.
 //
 // Twiddles are double precision: the radix-32 stage's and the DFT-16's
 // constants as literals, the first radix-16 stage's (w_512^(r k)) from an LDS
@@ -38,7 +41,7 @@
 // w_8192^k and w_8192^(4k) of the thread (two L1 loads per transform) and
 // their products.  Parity bar: the f64 bars of DESIGN.md "Oracle and parity"
 // (same decisions and stopping iterations as the staged engine and the CPU
-// restatement, NMSE within 1e-9).
+// restatement, NMSE within 1e-9; tests/test_amp_cw2d_gpu.py).
 #include "amp.hpp"
 
 namespace sg {
@@ -53,6 +56,11 @@ constexpr int D_T = CW2_THREADS;  // 512
 #define D_ABL 0
 #endif
 #define D_SKIP(bit) ((D_ABL & (bit)) != 0)
+// Az: the rows' class-invariant tables requested at the end of the previous class (1: 84 loop-carried
+// VGPRs, 68 spilled, Az 1.05 -> 1.93 ms per launch) or at the rows (0)
+#ifndef D_AZPF
+#define D_AZPF 0
+#endif
 constexpr int D_P = 8192;
 constexpr int D_SC = 9, D_NC = 2, D_SN = D_SC * D_NC;  // 18 class entries per thread (CW2_SLICE / 512)
 static_assert(D_SN * D_T == CW2_SLICE, "class slices of 18 entries per thread");
@@ -67,15 +75,14 @@ __device__ __forceinline__ dlds *d_re(uint32_t idx) { return (dlds *)(size_t)(8u
 
 // LDS layout, complex (16-byte) positions
 constexpr int D_IMG = c2pos(D_P);           // 8448: the padded image, element i at c2pos(i)
-constexpr int D_STAT = D_IMG;               // [1024] (max / tau, 1 / sum) of the previous beta (cw2d_ab)
-constexpr int D_TRASH = D_STAT + 1024;      // one complex slot: writes of padded entries and unused rows
+constexpr int D_TRASH = D_IMG + 1024;       // one complex slot: writes of padded entries and unused rows (where
+                                            // the class tables' trash index puts it: after the image and the
+                                            // f32 engine's section statistics, amp_cw2.hip)
 static_assert(16 * D_TRASH == 8 * (int)CW2_TRASH, "the class tables' trash index lands on the trash slot");
 constexpr int D_TW1 = D_TRASH + 1;          // [15][32] w_512^(r k) of the first radix-16 stage
 constexpr int D_CP_BYTES = 16 * (D_TW1 + 15 * 32);
 constexpr int D_LDS_BYTES = D_CP_BYTES + 4 * 72;  // + the class pointers (Q + 1 <= 72)
 static_assert(D_LDS_BYTES <= 160 * 1024, "LDS budget");
-constexpr uint32_t D_SEGMAX = D_SN * D_T;   // real index: segment max / tau of each section (cw2d_az,
-                                            // after the class copy inside the image)
 
 __device__ __forceinline__ int d_opaque(int v) {
     asm volatile("" : "+v"(v));
@@ -336,16 +343,14 @@ __device__ __forceinline__ double d_arg(double v, double ms, double tau, double 
 }  // namespace
 
 // ---------------------------------------------------------------------------- Ab
+// beta of the class in class order comes from cw2d_stats (tb.beta): no exponentials and no section
+// statistics here
 template <int OT>
 __global__ __launch_bounds__(D_T, 1) void cw2d_ab(Cw2dTables tb, RegBufs<double> bf) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int h = blockIdx.x & 1, cw = blockIdx.x >> 1, tid = threadIdx.x;
     if (!bf.active[cw]) return;
-    const size_t lb = (size_t)cw * tb.L;
-    const double tau = bf.tau[cw], inv_tau = 1.0 / tau;
-    for (int l = tid; l < tb.L; l += D_T)  // previous beta's section max / tau (amp_fused.hip sm_stage), 1 / sum
-        *d_at(D_STAT + l) = d2{bf.stM[lb + l] / tau, bf.stI[lb + l]};
-    double *s = bf.s + (size_t)cw * tb.LM;  // s in; beta out (cw2d_az's beta_prev)
+    const double *beta = tb.beta + (size_t)cw * tb.LM;
     const int Qh = tb.Q >> 1, mlo = h * Qh, mhi = mlo + Qh;
     d2 Ha[OT], Hb[OT];
 #pragma unroll
@@ -354,10 +359,13 @@ __global__ __launch_bounds__(D_T, 1) void cw2d_ab(Cw2dTables tb, RegBufs<double>
     const int *cpl = d_stage_cp(smem, tb, tid);
     __syncthreads();
     const __amdgpu_buffer_rsrc_t rk = d_rsrc(tb.ka, 4 * OT * D_T), rS = d_rsrc(tb.sa, 16 * OT * D_T);
-    // the thread's slot words and S = w_N2^a (reloaded per class from L1 / L2: held across the
-    // transform beside H they spill), slot-major: every load a contiguous run of the wavefront's lanes
-    // (thread-major rows of 12 complex doubles put each lane on its own cache lines: profiles/r05_f64_ablation.txt)
-    auto acc_tables = [&](int tl, uint32_t *ka, d2 *S) {
+    // the thread's slot words and S = w_N2^a, slot-major: every load a contiguous run of the wavefront's
+    // lanes (thread-major rows of 12 complex doubles put each lane on its own cache lines:
+    // profiles/r05_f64_ablation.txt); class-invariant, so requested after each transform and in flight
+    // during the loop edge and the next slice's requests
+    uint32_t ka[OT];
+    d2 S[OT];
+    auto acc_tables = [&](int tl) {
 #pragma unroll
         for (int j = 0; j < OT; ++j) {
             ka[j] = __builtin_amdgcn_raw_buffer_load_b32(rk, 4 * tl, 4 * j * D_T, 0);
@@ -367,7 +375,7 @@ __global__ __launch_bounds__(D_T, 1) void cw2d_ab(Cw2dTables tb, RegBufs<double>
     // Horner step of class m's transform (still in the image) for every owned output
     // (four slots' image reads at a time: all of them in flight beside H, S and the next class's slice
     // spill)
-    auto accumulate = [&](const uint32_t *ka, const d2 *S) {
+    auto accumulate = [&]() {
 #pragma unroll
         for (int j0 = 0; j0 < OT; j0 += 4) {
 #pragma unroll
@@ -384,13 +392,10 @@ __global__ __launch_bounds__(D_T, 1) void cw2d_ab(Cw2dTables tb, RegBufs<double>
         const int tl = d_opaque(tid);
         const int q0 = d_uni(cpl[m2]), q1 = d_uni(cpl[m2 + 1]);
         const bool prev = m2 < mhi - 1;
-        uint32_t ka[OT];
-        d2 S[OT];
-        if (prev) acc_tables(tl, ka, S);  // (first: vector-memory loads complete in order)
         double v[D_SN];
         uint32_t e[D_SN];
-        const __amdgpu_buffer_rsrc_t rs = d_rsrc(s + q0, 8 * (q1 - q0));  // past the class's end: 0 / dropped
         {
+            const __amdgpu_buffer_rsrc_t rb = d_rsrc(beta + q0, 8 * (q1 - q0));  // past the class's end: 0
             const __amdgpu_buffer_rsrc_t re = d_rsrc(tb.cls2 + (size_t)m2 * CW2_SLICE, 4 * CW2_SLICE);
 #pragma unroll
             for (int i = 0; i < D_SN; ++i) {
@@ -399,31 +404,23 @@ __global__ __launch_bounds__(D_T, 1) void cw2d_ab(Cw2dTables tb, RegBufs<double>
                     e[i] = (uint32_t)(((tl * 37 + i * 4099) & 8191) * 2);
                     continue;
                 }
-                v[i] = d_ldd(rs, 8 * tl + 8 * i * D_T, 0);
+                v[i] = d_ldd(rb, 8 * tl + 8 * i * D_T, 0);
                 e[i] = __builtin_amdgcn_raw_buffer_load_b32(re, 4 * tl, 4 * i * D_T, 0);
             }
         }
         const uint32_t cmk = tb.cmask[m2 * D_T + tl];
         if (prev && !D_SKIP(2)) {
-            accumulate(ka, S);
+            if (prev) accumulate();
             __syncthreads();  // the image is read before the scatter overwrites it
         }
 #pragma unroll
-        for (int i = 0; i < D_SN; ++i) {  // beta = eta(s), sparc.py:429-432 (padded entries: the trash slot)
-            const d2 mi = *d_at(D_STAT + (int)(e[i] >> 16));
-            const double b = (D_SKIP(8) ? v[i] : exp(d_arg(v[i], mi.x, tau, inv_tau))) * mi.y;
-            if (!D_SKIP(32)) *d_re(e[i] & 0xffffu) = b;
-            if (!D_SKIP(16)) d_std(rs, b, 8 * tl + 8 * i * D_T, 0);
-        }
+        for (int i = 0; i < D_SN; ++i)  // beta scattered into the image (padded entries: the trash slot)
+            if (!D_SKIP(32)) *d_re(e[i] & 0xffffu) = v[i];
         __syncthreads();
         if (!D_SKIP(1)) d_fft<false>(tl, cmk, tb.twp);
+        acc_tables(d_opaque(tid));
     }
-    {
-        uint32_t ka[OT];
-        d2 S[OT];
-        acc_tables(d_opaque(tid), ka, S);
-        accumulate(ka, S);
-    }
+    accumulate();
     // this half's part of the forward output Re(c1 H[a] + c2 conj H[b]), H = S^mlo (Horner sums)
     const __amdgpu_buffer_rsrc_t rc = d_rsrc(tb.cf, 32 * OT * D_T);
     double *xr = tb.xr + ((size_t)cw * 2 + h) * OT * D_T;
@@ -431,7 +428,7 @@ __global__ __launch_bounds__(D_T, 1) void cw2d_ab(Cw2dTables tb, RegBufs<double>
     for (int j = 0; j < OT; ++j) {
         d2 ha = Ha[j], hb = Hb[j];
         if (mlo > 0) {
-            const d2 w0 = d_pow(d_ld2(rS, 16 * tid, 16 * j * D_T), mlo);
+            const d2 w0 = d_pow(S[j], mlo);
             ha = dmul(ha, w0);
             hb = dmul(hb, w0);
         }
@@ -539,28 +536,22 @@ __global__ __launch_bounds__(D_T) void cw2d_ctrl(Cw2dTables tb, RegBufs<double> 
 }
 
 // ---------------------------------------------------------------------------- Az
+// rows -> inverse transform -> s = beta_prev + tau u, stored in class order; the section statistics are
+// cw2d_stats' (a separate launch at full occupancy: inside this one-workgroup-per-CU kernel they took
+// half its time, profiles/r05_f64_ablation.txt)
 template <int OT>
 __global__ __launch_bounds__(D_T, 1) void cw2d_az(Cw2dTables tb, RegBufs<double> bf, int t) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int h = blockIdx.x & 1, cw = blockIdx.x >> 1, tid = threadIdx.x;
     if (!bf.active[cw]) return;
-    const size_t lb = (size_t)cw * tb.L;
     const bool have_beta = t > 0;
-    const double tau = bf.tau[cw], inv_tau = 1.0 / tau;
+    const double tau = bf.tau[cw];
     double *s = bf.s + (size_t)cw * tb.LM;
+    const double *beta = tb.beta + (size_t)cw * tb.LM;
     const double *vz = tb.vz + (size_t)cw * OT * D_T;
-    const int Lb = tb.Lblk;
     const int Qh = tb.Q >> 1, mlo = h * Qh, mhi = mlo + Qh;
-    // running statistics of sections tid and tid + 512 over this half's classes
-    double Mr[2] = {-INFINITY, -INFINITY}, R1[2] = {0.0, 0.0}, R2[2] = {0.0, 0.0}, st[2] = {NAN, NAN};
-    int jt[2] = {-1, -1};
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int sec = tid + k * D_T;
-        if (bf.true_idx && sec < Lb) jt[k] = tb.qpos[sec * tb.M + bf.true_idx[lb + sec]];
-    }
     const __amdgpu_buffer_rsrc_t rS = d_rsrc(tb.sa, 16 * OT * D_T);
-    d2 W[OT];  // w_N2^(m a) of the class, rotated by S = w_N2^a per class (S reloaded per class)
+    d2 W[OT];  // w_N2^(m a) of the class, rotated by S = w_N2^a per class
 #pragma unroll
     for (int j = 0; j < OT; ++j) W[j] = d_pow(d_ld2(rS, 16 * tid, 16 * j * D_T), mlo);
     d_tw1_init<true>(tid, tb.twp);
@@ -568,24 +559,28 @@ __global__ __launch_bounds__(D_T, 1) void cw2d_az(Cw2dTables tb, RegBufs<double>
     __syncthreads();
     const __amdgpu_buffer_rsrc_t rv = d_rsrc(vz, 8 * OT * D_T), rk = d_rsrc(tb.ka, 4 * OT * D_T),
                                  rg = d_rsrc(tb.gf, 32 * OT * D_T);
+    // the rows' slot words, z / phi and S are class-invariant: requested at the end of the previous class
+    uint32_t kall[OT];
+    double vall[OT];
+    d2 S[OT];
+    auto rows_tables = [&](int tl) {
+#pragma unroll
+        for (int j = 0; j < OT; ++j) {
+            kall[j] = __builtin_amdgcn_raw_buffer_load_b32(rk, 4 * tl, 4 * j * D_T, 0);
+            vall[j] = d_ldd(rv, 8 * tl, 8 * j * D_T);
+            S[j] = d_ld2(rS, 16 * tl, 16 * j * D_T);
+        }
+    };
+    if (D_AZPF) rows_tables(tid);
     for (int m2 = mlo; m2 < mhi; ++m2) {
         const int tl = d_opaque(tid);
         const uint32_t rmk = tb.cmask[tb.Q * D_T + tl];
         const int q0 = d_uni(cpl[m2]), q1 = d_uni(cpl[m2 + 1]);
-        const __amdgpu_buffer_rsrc_t rs = d_rsrc(s + q0, 8 * (q1 - q0));
         if (!D_SKIP(128)) {
+            if (!D_AZPF) rows_tables(tl);
             // rows r and P - r of each owned pair: sums of al v conj(W) / be v W over its outputs (v = z / phi),
             // branch-free as amp_cw2.hip's rows (NEWROW restarts the sums; both rows written on the pair's last
             // slot, the trash slot otherwise; r = 0, P / 2: the sum at row r)
-            uint32_t kall[OT];
-            double vall[OT];
-            d2 S[OT];
-#pragma unroll
-            for (int j = 0; j < OT; ++j) {  // (slot-major: contiguous per wavefront, see cw2d_ab)
-                kall[j] = __builtin_amdgcn_raw_buffer_load_b32(rk, 4 * tl, 4 * j * D_T, 0);
-                vall[j] = d_ldd(rv, 8 * tl, 8 * j * D_T);
-                S[j] = d_ld2(rS, 16 * tl, 16 * j * D_T);
-            }
             constexpr int CH = 4;  // slots per round of coefficient loads
             d2 u0{0.0, 0.0}, u1{0.0, 0.0};
 #pragma unroll
@@ -619,6 +614,7 @@ __global__ __launch_bounds__(D_T, 1) void cw2d_az(Cw2dTables tb, RegBufs<double>
         double v[D_SN];
         uint32_t e[D_SN];
         {
+            const __amdgpu_buffer_rsrc_t rb = d_rsrc(beta + q0, 8 * (q1 - q0));
             const __amdgpu_buffer_rsrc_t re = d_rsrc(tb.cls2 + (size_t)m2 * CW2_SLICE, 4 * CW2_SLICE);
 #pragma unroll
             for (int i = 0; i < D_SN; ++i) {
@@ -628,158 +624,137 @@ __global__ __launch_bounds__(D_T, 1) void cw2d_az(Cw2dTables tb, RegBufs<double>
                     continue;
                 }
                 e[i] = __builtin_amdgcn_raw_buffer_load_b32(re, 4 * tl, 4 * i * D_T, 0);
-                v[i] = d_ldd(rs, 8 * tl + 8 * i * D_T, 0);  // (t = 0: unused)
-            }
-        }
-        int sa[2], sb[2];  // the sections' segments of the class (past Lb: empty)
-        {
-            const __amdgpu_buffer_rsrc_t rq = d_rsrc(tb.seg + (size_t)m2 * (Lb + 1), 2 * (Lb + 1));
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const int sec = tl + k * D_T;
-                sa[k] = __builtin_amdgcn_raw_buffer_load_b16(rq, 2 * sec, 0, 0);
-                sb[k] = __builtin_amdgcn_raw_buffer_load_b16(rq, 2 * sec + 2, 0, 0);
+                v[i] = have_beta ? d_ldd(rb, 8 * tl + 8 * i * D_T, 0) : 0.0;
             }
         }
         __syncthreads();
         if (!D_SKIP(64)) d_fft<true>(tl, rmk, tb.twp);
-        double snv[D_SN];
+        {
+            const __amdgpu_buffer_rsrc_t rs = d_rsrc(s + q0, 8 * (q1 - q0));  // past the class's end: dropped
 #pragma unroll
-        for (int i = 0; i < D_SN; ++i) {  // s = beta_prev + tau u (sparc.py:972); beta_prev stored by cw2d_ab
-            const double b = have_beta ? v[i] : 0.0;
-            snv[i] = b + tau * *d_re(e[i] & 0xffffu);
-        }
-#pragma unroll
-        for (int c = 0; c < D_SN; ++c)  // s to HBM (class order)
-            if (!D_SKIP(1024)) d_std(rs, snv[c], 8 * tl + 8 * c * D_T, 0);
-        __syncthreads();
-#pragma unroll
-        for (int c = 0; c < D_SN; ++c) *d_re(tl + c * D_T) = snv[c];  // s of the class in class order
-        __syncthreads();
-        // section statistics of the class (the reference's two-pass softmax sums, sparc.py:429-432):
-        // (1) each section's segment maximum, one thread per section; (2) e = exp(s / tau - max / tau)
-        // of the thread's own entries (one exponential per entry, not one per entry of the longest
-        // segment of the wavefront); (3) the segment sums of e and e^2, merged into the running statistics
-        // (segments average LM / (Q L) = 8 entries: the first 16 are read unconditionally -- inside the
-        // image past the segment too -- and masked, one LDS round trip; longer ones loop)
-        constexpr int RC = 16;
-        double msg[2];
-#pragma unroll
-        for (int k = 0; k < (D_SKIP(512) ? 0 : 2); ++k) {
-            const int a = sa[k], n = sb[k] - sa[k];
-            double x[RC];
-#pragma unroll
-            for (int i = 0; i < RC; ++i) x[i] = d_keep(*d_re(a + i), i, n, 0xfff00000u);  // past the end: -inf
-            double m = x[0];
-#pragma unroll
-            for (int i = 1; i < RC; ++i) m = fmax(m, x[i]);
-            for (int c = RC; c < n; ++c) m = fmax(m, *d_re(a + c));
-            msg[k] = m;
-            const int sec = tl + k * D_T;
-            if (n > 0) *d_re(D_SEGMAX + sec) = m / tau;  // (amp_fused.hip sm_stage)
-            if (jt[k] >= q0 && jt[k] < q1) st[k] = *d_re(jt[k] - q0);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int c = 0; c < D_SN; ++c) {  // (padded entries: section 0, their values unread)
-            if (D_SKIP(512)) break;
-            const double ms = *d_re(D_SEGMAX + (e[c] >> 16));
-            *d_re(tl + c * D_T) = D_SKIP(2048) ? snv[c] - ms : exp(d_arg(snv[c], ms, tau, inv_tau));
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < (D_SKIP(512) ? 0 : 2); ++k) {
-            const int a = sa[k], n = sb[k] - sa[k];
-            if (n <= 0) continue;
-            double S1 = 0.0, S2 = 0.0;
-            double x[RC];
-#pragma unroll
-            for (int i = 0; i < RC; ++i) x[i] = d_keep(*d_re(a + i), i, n, 0u);  // past the end: 0
-#pragma unroll
-            for (int i = 0; i < RC; ++i) {
-                S1 += x[i];
-                S2 = __builtin_fma(x[i], x[i], S2);
-            }
-            for (int c = RC; c < n; ++c) {
-                const double e1 = *d_re(a + c);
-                S1 += e1;
-                S2 = __builtin_fma(e1, e1, S2);
-            }
-            const double m = msg[k];
-            // the staged merge's factor exp(m_c / tau - M / tau) (amp_fused.hip sm_arg), both quotients by
-            // the Markstein division (an empty running maximum: factor 0)
-            const double qm = d_arg(m, 0.0, tau, inv_tau), qr = d_arg(Mr[k], 0.0, tau, inv_tau);
-            if (m > Mr[k]) {
-                const double f = Mr[k] == -INFINITY ? 0.0 : exp(qr - qm);
-                R1[k] = R1[k] * f + S1;
-                R2[k] = R2[k] * (f * f) + S2;
-                Mr[k] = m;
-            } else {
-                const double f = exp(qm - qr);
-                R1[k] += S1 * f;
-                R2[k] += S2 * (f * f);
+            for (int i = 0; i < D_SN; ++i) {  // s = beta_prev + tau u (sparc.py:972), class order
+                const double sv = v[i] + tau * *d_re(e[i] & 0xffffu);
+                if (!D_SKIP(1024)) d_std(rs, sv, 8 * tl + 8 * i * D_T, 0);
             }
         }
+        if (D_AZPF && m2 + 1 < mhi) rows_tables(tl);
         __syncthreads();  // the next class overwrites the image
-    }
-    double *part = tb.part + ((size_t)cw * 2 + h) * Lb * 4;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int sec = tid + k * D_T;
-        if (sec < Lb) {
-            d2 *p2 = reinterpret_cast<d2 *>(part + 4 * (size_t)sec);
-            p2[0] = d2{Mr[k], R1[k]};
-            p2[1] = d2{R2[k], st[k]};
-        }
     }
 }
 
-// ---------------------------------------------------------------------------- merge
-// The halves' statistics per section as the staged engine's reg_merge (f64: sums with the maximum's
-// term, psi = 1 - mean of S2 / S1^2), then psi, NMSE and the stopping rule (sparc.py:973-988)
-__global__ __launch_bounds__(1024) void cw2d_merge(Cw2dTables tb, RegBufs<double> bf, AmpScalars sc, AmpParams pr,
+// ---------------------------------------------------------------------------- statistics
+// After Az: per section, the softmax of s over its M entries (sparc.py:429-432, the staged engine's
+// argument x / tau - max / tau), its statistics and beta itself (class order, tb.beta: the next Ab's
+// input and the next Az's beta_prev), the previous beta's section max and 1 / sum for a hand-over
+// (stM, stI) and the section's sum beta^2 and squared error (sparc.py:973-981) for cw2d_final.
+// One wavefront per section (a segment of it per class: a contiguous run of s in class order, about
+// LM / (Q L) = 8 entries; Q <= 64): every entry read once from HBM, one exponential per entry (and
+// per padding slot of a segment under 16), sums in a fixed order (per lane, then a xor-shuffle tree).
+constexpr int ST_WAVES = 4;  // sections per 256-thread workgroup
+constexpr int ST_RND = 8;    // rounds of eight segments (Q <= 64 classes)
+__device__ __forceinline__ double d_wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ double d_wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__global__ __launch_bounds__(64 * ST_WAVES) void cw2d_stats(Cw2dTables tb, RegBufs<double> bf) {
+    const int wpc = tb.L / ST_WAVES;  // workgroups per codeword
+    const int cw = blockIdx.x / wpc, l = (blockIdx.x % wpc) * ST_WAVES + (int)(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, g = lane >> 3, i0 = lane & 7;
+    if (!bf.active[cw]) return;
+    const size_t lb = (size_t)cw * tb.L;
+    const double tau = bf.tau[cw], inv_tau = 1.0 / tau;
+    const double *s = bf.s + (size_t)cw * tb.LM;
+    double *beta = tb.beta + (size_t)cw * tb.LM;
+    // eight lanes per segment, eight segments (classes 8 r + g) per round: entries i0 and i0 + 8 of each,
+    // so a load instruction reads eight contiguous runs (with one lane per segment, every lane of every
+    // load was a cache line of its own: the launch took 1.2 ms per iteration); indices clamped into the
+    // segment (entry 0 of an empty one) and the values past its end masked
+    int p0[ST_RND], n[ST_RND];
+#pragma unroll
+    for (int r = 0; r < ST_RND; ++r) {
+        const int m = ST_RND * r + g;
+        p0[r] = 0;
+        n[r] = 0;
+        if (m < tb.Q) {
+            const uint16_t *sg = tb.seg + (size_t)m * (tb.Lblk + 1);
+            p0[r] = tb.cls_ptr[m] + sg[l];
+            n[r] = sg[l + 1] - sg[l];
+        }
+    }
+    double x[2 * ST_RND];
+#pragma unroll
+    for (int r = 0; r < ST_RND; ++r) {
+        const int nl = n[r] > 0 ? n[r] - 1 : 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)  // past the end: -inf
+            x[2 * r + h] = d_keep(s[p0[r] + min(i0 + 8 * h, nl)], i0 + 8 * h, n[r], 0xfff00000u);
+    }
+    double m = x[0];
+#pragma unroll
+    for (int i = 1; i < 2 * ST_RND; ++i) m = fmax(m, x[i]);
+#pragma unroll
+    for (int r = 0; r < ST_RND; ++r)
+        for (int i = i0 + 16; i < n[r]; i += 8) m = fmax(m, s[p0[r] + i]);  // (segments over 16: rare)
+    const double M = d_wave_max(m);
+    const double ms = M / tau;  // (amp_fused.hip sm_stage)
+    double S1 = 0.0, S2 = 0.0;
+#pragma unroll
+    for (int r = 0; r < ST_RND; ++r)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {  // past the end: 0 (the Markstein quotient of -inf is NaN)
+            const int k = 2 * r + h;
+            x[k] = d_keep(exp(d_arg(x[k], ms, tau, inv_tau)), i0 + 8 * h, n[r], 0u);
+            S1 += x[k];
+            S2 = __builtin_fma(x[k], x[k], S2);
+        }
+#pragma unroll
+    for (int r = 0; r < ST_RND; ++r)
+        for (int i = i0 + 16; i < n[r]; i += 8) {
+            const double e1 = exp(d_arg(s[p0[r] + i], ms, tau, inv_tau));
+            S1 += e1;
+            S2 = __builtin_fma(e1, e1, S2);
+        }
+    S1 = d_wave_sum(S1);
+    S2 = d_wave_sum(S2);
+    const double inv = 1.0 / S1;
+#pragma unroll
+    for (int r = 0; r < ST_RND; ++r) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            if (i0 + 8 * h < n[r]) beta[p0[r] + i0 + 8 * h] = x[2 * r + h] * inv;
+        for (int i = i0 + 16; i < n[r]; i += 8) beta[p0[r] + i] = exp(d_arg(s[p0[r] + i], ms, tau, inv_tau)) * inv;
+    }
+    if (lane == 0) {
+        bf.stM[lb + l] = M;
+        bf.stI[lb + l] = inv;
+        const double ss = S2 * inv * inv;
+        double err = ss;
+        if (bf.true_idx) {
+            const double st = s[tb.qpos[l * tb.M + bf.true_idx[lb + l]]];
+            err = ss - 2.0 * (exp(st / tau - M / tau) * inv) + 1.0;
+        }
+        tb.sec[(lb + l) * 2] = ss;
+        tb.sec[(lb + l) * 2 + 1] = err;
+    }
+}
+
+// psi, NMSE and the stopping rule from the sections' sums (sparc.py:973-988), fixed summation order
+__global__ __launch_bounds__(1024) void cw2d_final(Cw2dTables tb, RegBufs<double> bf, AmpScalars sc, AmpParams pr,
                                                    int t) {
     __shared__ double red[16];
     const int cw = blockIdx.x, tid = threadIdx.x;
     if (!bf.active[cw]) return;
     const size_t lb = (size_t)cw * tb.L;
-    const int Lb = tb.Lblk;
-    const double tau = bf.tau[cw];
     double a = 0.0, er = 0.0;
-    if (tid < Lb) {
-        const double *part = tb.part + (size_t)cw * 2 * Lb * 4;
-        double mh[2], s1[2], s2[2], sth[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const d2 *p2 = reinterpret_cast<const d2 *>(part + ((size_t)h * Lb + tid) * 4);
-            const d2 x = p2[0], y = p2[1];
-            mh[h] = x.x;
-            s1[h] = x.y;
-            s2[h] = y.x;
-            sth[h] = y.y;
-        }
-        const double M = fmax(mh[0], mh[1]);
-        double S1 = 0.0, S2 = 0.0, s_true = NAN;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if (!(sth[h] != sth[h])) s_true = sth[h];
-            if (s1[h] > 0.0) {
-                const double f = exp(mh[h] / tau - M / tau);
-                S1 += s1[h] * f;
-                S2 += s2[h] * (f * f);
-            }
-        }
-        const double inv = 1.0 / S1;
-        bf.stM[lb + tid] = M;
-        bf.stI[lb + tid] = inv;
-        const double ss = S2 * inv * inv;
-        double err = ss;
-        if (bf.true_idx) {
-            const double bt = exp(s_true / tau - M / tau) * inv;
-            err = ss - 2.0 * bt + 1.0;
-        }
-        a = ss;
-        er = err;
+    for (int l = tid; l < tb.L; l += 1024) {
+        a += tb.sec[(lb + l) * 2];
+        er += tb.sec[(lb + l) * 2 + 1];
     }
     a = d_block_sum(a, red);
     er = d_block_sum(er, red);
@@ -836,7 +811,8 @@ static int cw2d_launch(const Cw2dTables &tb, const RegBufs<double> &bf, const Am
     }
     {
         ProfScope ps(SG_PH_CW2_CTRL, s);
-        hipLaunchKernelGGL((cw2d_merge), gB, dim3(1024), 0, s, tb, bf, sc, pr, t);
+        hipLaunchKernelGGL((cw2d_stats), dim3(bf.B * (tb.L / ST_WAVES)), dim3(64 * ST_WAVES), 0, s, tb, bf);
+        hipLaunchKernelGGL((cw2d_final), gB, dim3(1024), 0, s, tb, bf, sc, pr, t);
     }
     return SG_OK;
 }
@@ -844,8 +820,8 @@ static int cw2d_launch(const Cw2dTables &tb, const RegBufs<double> &bf, const Am
 int cw2d_launch_iter(const Cw2dTables &tb, const RegBufs<double> &bf, const AmpScalars &sc, const AmpParams &pr,
                      int t, hipStream_t s) {
     if (bf.B <= 0) return SG_OK;
-    if (tb.Q % 2 || tb.L > 1024 || tb.Lblk > 2 * D_T || tb.maxcls > CW2_SLICE || tb.N2 != D_P * tb.Q ||
-        tb.Q > 71 || tb.M <= 0)
+    if (tb.Q % 2 || tb.Q > 64 || tb.L > 1024 || tb.L % ST_WAVES || tb.Lblk != tb.L || tb.maxcls > CW2_SLICE ||
+        tb.N2 != D_P * tb.Q || tb.M <= 0)
         return fail(SG_ERR_UNSUPPORTED, "f64 split engine: sizes outside its compile-time bounds");
     ProfScope ps(SG_PH_AMP_CW, s);
     switch (tb.OT) {

@@ -81,6 +81,7 @@ struct sg_amp_plan {
     // its double-precision form (amp_cw2d.hip): coefficients, the slots' w_N2^a, the P-point twiddles
     double *c2d_cf = nullptr, *c2d_gf = nullptr, *c2d_sa = nullptr, *c2d_twp = nullptr;
     void *ws_c2xp = nullptr, *ws_c2vz = nullptr, *ws_c2part = nullptr, *ws_c2ys = nullptr, *ws_c2zs = nullptr;
+    void *ws_c2beta = nullptr, *ws_c2sec = nullptr;  // f64 form: beta in class order, per-section sums
     uint16_t *c_cmask = nullptr;  // [Q + 1][1024] per-codeword engine: written image values per thread
     int32_t *c_oa = nullptr, *c_ob = nullptr, *c_gi = nullptr;
     void *c_gc = nullptr, *c_stw = nullptr;
@@ -189,7 +190,7 @@ static int plan_free_ws(sg_amp_plan *p) {
                    (void **)&p->ws_bco, (void **)&p->ws_nmse, (void **)&p->ws_active, (void **)&p->ws_argmax,
                    (void **)&p->ws_true, (void **)&p->ws_tfinal, &p->ws_s, &p->ws_tu, &p->ws_xn, &p->ws_part,
                    &p->ws_stM, &p->ws_stI, (void **)&p->ws_tau_prev, &p->ws_gbuf, &p->ws_c2xp, &p->ws_c2vz, &p->ws_c2ys, &p->ws_c2zs,
-                   &p->ws_c2part};
+                   &p->ws_c2part, &p->ws_c2beta, &p->ws_c2sec};
     for (void **x : ws) {
         if (*x) hipFree(*x);
         *x = nullptr;
@@ -226,6 +227,10 @@ static int ensure_ws(sg_amp_plan *p, int B, int t_max) {
             SG_ALLOC(p->ws_c2ys, Bz * p->cw2OT * CW2_THREADS * rs);
             SG_ALLOC(p->ws_c2zs, Bz * p->cw2OT * CW2_THREADS * rs);
             SG_ALLOC(p->ws_c2part, Bz * 2 * p->Lblk * 4 * rs);
+            if (p->precision == SG_F64) {
+                SG_ALLOC(p->ws_c2beta, Bz * p->LM * rs);
+                SG_ALLOC(p->ws_c2sec, Bz * p->L * 2 * rs);
+            }
         }
         SG_ALLOC(p->ws_stM, Bz * p->L * rs);
         SG_ALLOC(p->ws_stI, Bz * p->L * rs);
@@ -969,7 +974,7 @@ static Cw2dTables c2dtables(const sg_amp_plan *p) {
     tb.cf = p->c2d_cf; tb.gf = p->c2d_gf; tb.sa = p->c2d_sa; tb.twp = p->c2d_twp;
     tb.cls_ptr = p->r_cls_ptr; tb.cls2 = p->c2_cls; tb.qpos = p->r_qpos; tb.seg = p->r_seg;
     tb.xr = (double *)p->ws_c2xp; tb.vz = (double *)p->ws_c2vz; tb.ys = (double *)p->ws_c2ys;
-    tb.zs = (double *)p->ws_c2zs; tb.part = (double *)p->ws_c2part;
+    tb.zs = (double *)p->ws_c2zs; tb.beta = (double *)p->ws_c2beta; tb.sec = (double *)p->ws_c2sec;
     return tb;
 }
 
