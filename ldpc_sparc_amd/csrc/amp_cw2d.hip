@@ -648,10 +648,10 @@ __global__ __launch_bounds__(D_T, 1) void cw2d_az(Cw2dTables tb, RegBufs<double>
 // input and the next Az's beta_prev), the previous beta's section max and 1 / sum for a hand-over
 // (stM, stI) and the section's sum beta^2 and squared error (sparc.py:973-981) for cw2d_final.
 // One wavefront per section (a segment of it per class: a contiguous run of s in class order, about
-// LM / (Q L) = 8 entries; Q <= 64): every entry read once from HBM, one exponential per entry (and
-// per padding slot of a segment under 16), sums in a fixed order (per lane, then a xor-shuffle tree).
+// LM / (Q L) = 8 entries; Q <= 64, M <= 512): every entry read once from HBM, one exponential per
+// entry, sums in a fixed order (per lane, then a xor-shuffle tree).
 constexpr int ST_WAVES = 4;  // sections per 256-thread workgroup
-constexpr int ST_RND = 8;    // rounds of eight segments (Q <= 64 classes)
+constexpr int ST_K = 8;      // entries per lane: sections of M <= 512 entries
 __device__ __forceinline__ double d_wave_max(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
@@ -663,73 +663,68 @@ __device__ __forceinline__ double d_wave_sum(double v) {
     return v;
 }
 __global__ __launch_bounds__(64 * ST_WAVES) void cw2d_stats(Cw2dTables tb, RegBufs<double> bf) {
+    // per wavefront: exclusive prefix of the segment lengths over the classes, and each segment's base
+    // (class-order position minus that prefix): entry k of the section lives at base[m] + k, m the last
+    // class with prefix[m] <= k
+    __shared__ int pre[ST_WAVES][64], bas[ST_WAVES][64];
     const int wpc = tb.L / ST_WAVES;  // workgroups per codeword
-    const int cw = blockIdx.x / wpc, l = (blockIdx.x % wpc) * ST_WAVES + (int)(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63, g = lane >> 3, i0 = lane & 7;
+    const int w = (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int cw = blockIdx.x / wpc, l = (blockIdx.x % wpc) * ST_WAVES + w;
     if (!bf.active[cw]) return;
     const size_t lb = (size_t)cw * tb.L;
     const double tau = bf.tau[cw], inv_tau = 1.0 / tau;
     const double *s = bf.s + (size_t)cw * tb.LM;
     double *beta = tb.beta + (size_t)cw * tb.LM;
-    // eight lanes per segment, eight segments (classes 8 r + g) per round: entries i0 and i0 + 8 of each,
-    // so a load instruction reads eight contiguous runs (with one lane per segment, every lane of every
-    // load was a cache line of its own: the launch took 1.2 ms per iteration); indices clamped into the
-    // segment (entry 0 of an empty one) and the values past its end masked
-    int p0[ST_RND], n[ST_RND];
-#pragma unroll
-    for (int r = 0; r < ST_RND; ++r) {
-        const int m = ST_RND * r + g;
-        p0[r] = 0;
-        n[r] = 0;
-        if (m < tb.Q) {
-            const uint16_t *sg = tb.seg + (size_t)m * (tb.Lblk + 1);
-            p0[r] = tb.cls_ptr[m] + sg[l];
-            n[r] = sg[l + 1] - sg[l];
-        }
+    int p0 = 0, n = 0;
+    if (lane < tb.Q) {
+        const uint16_t *sg = tb.seg + (size_t)lane * (tb.Lblk + 1);
+        p0 = tb.cls_ptr[lane] + sg[l];
+        n = sg[l + 1] - sg[l];
     }
-    double x[2 * ST_RND];
+    int inc = n;  // inclusive scan over the lanes
 #pragma unroll
-    for (int r = 0; r < ST_RND; ++r) {
-        const int nl = n[r] > 0 ? n[r] - 1 : 0;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
+    }
+    const int total = __shfl(inc, 63, 64);  // the section's entries (M)
+    pre[w][lane] = inc - n;
+    bas[w][lane] = p0 - (inc - n);
+    __syncthreads();
+    // the section's entries k = lane + 64 j in concatenated class order: consecutive lanes read consecutive
+    // positions of a segment (coalesced runs), no padding, one exponential per entry
+    const int nq = tb.Q;
+    int ad[ST_K];
+    double x[ST_K];
 #pragma unroll
-        for (int h = 0; h < 2; ++h)  // past the end: -inf
-            x[2 * r + h] = d_keep(s[p0[r] + min(i0 + 8 * h, nl)], i0 + 8 * h, n[r], 0xfff00000u);
+    for (int j = 0; j < ST_K; ++j) {
+        const int k = lane + 64 * j;
+        int lo = 0;
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1)  // last class with pre <= k (empty classes: same pre)
+            if (lo + step < nq && pre[w][lo + step] <= k) lo += step;
+        const bool in = k < total;
+        ad[j] = in ? bas[w][lo] + k : 0;
+        x[j] = d_keep(s[ad[j]], k, total, 0xfff00000u);  // past the section: -inf
     }
     double m = x[0];
 #pragma unroll
-    for (int i = 1; i < 2 * ST_RND; ++i) m = fmax(m, x[i]);
-#pragma unroll
-    for (int r = 0; r < ST_RND; ++r)
-        for (int i = i0 + 16; i < n[r]; i += 8) m = fmax(m, s[p0[r] + i]);  // (segments over 16: rare)
+    for (int j = 1; j < ST_K; ++j) m = fmax(m, x[j]);
     const double M = d_wave_max(m);
     const double ms = M / tau;  // (amp_fused.hip sm_stage)
     double S1 = 0.0, S2 = 0.0;
 #pragma unroll
-    for (int r = 0; r < ST_RND; ++r)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {  // past the end: 0 (the Markstein quotient of -inf is NaN)
-            const int k = 2 * r + h;
-            x[k] = d_keep(exp(d_arg(x[k], ms, tau, inv_tau)), i0 + 8 * h, n[r], 0u);
-            S1 += x[k];
-            S2 = __builtin_fma(x[k], x[k], S2);
-        }
-#pragma unroll
-    for (int r = 0; r < ST_RND; ++r)
-        for (int i = i0 + 16; i < n[r]; i += 8) {
-            const double e1 = exp(d_arg(s[p0[r] + i], ms, tau, inv_tau));
-            S1 += e1;
-            S2 = __builtin_fma(e1, e1, S2);
-        }
+    for (int j = 0; j < ST_K; ++j) {  // past the section: 0 (the Markstein quotient of -inf is NaN)
+        x[j] = d_keep(exp(d_arg(x[j], ms, tau, inv_tau)), lane + 64 * j, total, 0u);
+        S1 += x[j];
+        S2 = __builtin_fma(x[j], x[j], S2);
+    }
     S1 = d_wave_sum(S1);
     S2 = d_wave_sum(S2);
     const double inv = 1.0 / S1;
 #pragma unroll
-    for (int r = 0; r < ST_RND; ++r) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-            if (i0 + 8 * h < n[r]) beta[p0[r] + i0 + 8 * h] = x[2 * r + h] * inv;
-        for (int i = i0 + 16; i < n[r]; i += 8) beta[p0[r] + i] = exp(d_arg(s[p0[r] + i], ms, tau, inv_tau)) * inv;
-    }
+    for (int j = 0; j < ST_K; ++j)
+        if (lane + 64 * j < total) beta[ad[j]] = x[j] * inv;
     if (lane == 0) {
         bf.stM[lb + l] = M;
         bf.stI[lb + l] = inv;
@@ -821,6 +816,7 @@ int cw2d_launch_iter(const Cw2dTables &tb, const RegBufs<double> &bf, const AmpS
                      int t, hipStream_t s) {
     if (bf.B <= 0) return SG_OK;
     if (tb.Q % 2 || tb.Q > 64 || tb.L > 1024 || tb.L % ST_WAVES || tb.Lblk != tb.L || tb.maxcls > CW2_SLICE ||
+        tb.M > 64 * ST_K ||
         tb.N2 != D_P * tb.Q || tb.M <= 0)
         return fail(SG_ERR_UNSUPPORTED, "f64 split engine: sizes outside its compile-time bounds");
     ProfScope ps(SG_PH_AMP_CW, s);
