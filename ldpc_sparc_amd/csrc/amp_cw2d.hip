@@ -761,7 +761,7 @@ __global__ __launch_bounds__(1024) void cw2d_final(Cw2dTables tb, RegBufs<double
         *psi = pnew;
         nmse[t + 1] = er / denom;
         bool stop = false;
-        if (t > 0) {
+        if (t > 0 && D_ABL == 0) {  // (ablation builds never stop early: every launch does the same work)
             const double pp = *psi_prev;
             stop = fabs(pnew - pp) <= pr.atol + pr.rtol * fabs(pp);  // sparc.py:984-986
         }
