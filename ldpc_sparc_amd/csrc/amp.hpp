@@ -209,6 +209,9 @@ constexpr uint32_t CW2_TRASH = 2 * (8192 + 256) + 2048;  // LDS float index of t
 constexpr uint32_t CW_SELF = 1u << 23;  // the pair's two rows coincide (r = 0 or P / 2)
 // a thread's slots padded to a multiple of four (thread-major tables: 16-byte loads)
 __host__ __device__ constexpr int cw2_otp(int ot) { return (ot + 3) & ~3; }
+// z / phi thread-major (one load round of 16-byte loads in cw2_az) up to 12 slots per thread; above, cw2_az
+// loads the slots in two rounds of single words, slot-major
+__host__ __device__ constexpr bool cw2_vz_tm(int ot) { return ot <= 12; }
 struct Cw2Tables {
     int L, M, LM, n, N2, Q, Lblk, OT, maxcls;
     float inv_n2;             // 1 / N2
@@ -227,7 +230,8 @@ struct Cw2Tables {
     const uint2 *rab;         // [OT][512] LDS byte addresses of rows r, P - r of the slot's output (cw2_ab reads)
     const uint2 *wab;         // [OT][512] LDS byte addresses of the slot's row writes (rows r, P - r on the
                               // pair's last slot, else the trash slot; r = 0, P / 2: row r and trash)
-    float *vz;                // [B][512][OTP] z / phi in slot order, thread-major (OTP = OT rounded up to 4)
+    float *vz;                // z / phi in slot order: [B][512][OTP] thread-major (OTP = OT rounded up to 4) if
+                              // cw2_vz_tm(OT), else [B][OT][512]
     float *ys, *zs;           // [B][OT][512] y (copied at t = 0) and z in slot order (cw2_ctrl reads them
                               // coalesced; z in natural order is still written for a hand-over)
     float4 *part;             // [B][2][Lblk] partial section statistics (max, R1, R2, s of the true entry or NaN)

@@ -75,6 +75,10 @@ static_assert(C2_EPT == 16, "the transform is written for 16 values per thread")
 #ifndef C2_ROWS_DERIVE
 #define C2_ROWS_DERIVE 1
 #endif
+// Ab: the accumulation's slot words requested after each transform (1) or at the class start (0) (A/B)
+#ifndef C2_AB_PF
+#define C2_AB_PF 0
+#endif
 #ifndef C2_STAGGER_SEL
 #define C2_STAGGER_SEL 0
 #endif
@@ -430,6 +434,9 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
     // Software-pipelined over the classes: class m2's slice is requested, then the previous class's
     // transform (still in the image) is accumulated while the loads are in flight, then m2 is scattered
     // and transformed
+#if C2_AB_PF
+    uint32_t kapf[OT];
+#endif
     for (int m2 = h * Qh; m2 < (h + 1) * Qh; ++m2) {
         const int tl = c2_opaque(tid);
         C2_TPC(0);
@@ -444,8 +451,12 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
             __syncthreads();
         }
         // (the accumulation's table loads first: vector-memory loads complete in order)
+#if C2_AB_PF
+        uint32_t (&ka)[OT] = kapf;
+#else
         uint32_t ka[PL ? OT : 1];
         if (PL && m2 > h * Qh) acc_tables(tl, ka);
+#endif
         float v[C2_SN];
         uint32_t e[C2_SN];
         {  // every load of the class slice in one round trip; past the class's end s reads 0 and the
@@ -490,6 +501,9 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
         C2_TPC(3);
         if (!C2_SKIP(1)) c2_fft<false>(tl, cmk);
         C2_TPC(6);
+#if C2_AB_PF
+        acc_tables(c2_opaque(tid), kapf);  // class-invariant: in flight across the loop edge
+#endif
     }
     {
         uint32_t ka[OT];
@@ -605,13 +619,19 @@ __global__ __launch_bounds__(C2_T) void cw2_ctrl(Cw2Tables tb, RegBufs<float> bf
     }
     const float iph = (float)(1.0 / phi);
     constexpr int OTP = cw2_otp(OT);
-    float4 *vz4 = reinterpret_cast<float4 *>(tb.vz + ((size_t)cw * C2_T + tid) * OTP);  // thread-major
+    if constexpr (cw2_vz_tm(OT)) {
+        float4 *vz4 = reinterpret_cast<float4 *>(tb.vz + ((size_t)cw * C2_T + tid) * OTP);  // thread-major
 #pragma unroll
-    for (int q = 0; q < OTP / 4; ++q) {  // z / phi (sparc.py:972); padding slots 0
-        float w[4];
+        for (int q = 0; q < OTP / 4; ++q) {  // z / phi (sparc.py:972); padding slots 0
+            float w[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) w[c] = 4 * q + c < OT ? zr[4 * q + c] * iph : 0.f;
-        vz4[q] = make_float4(w[0], w[1], w[2], w[3]);
+            for (int c = 0; c < 4; ++c) w[c] = 4 * q + c < OT ? zr[4 * q + c] * iph : 0.f;
+            vz4[q] = make_float4(w[0], w[1], w[2], w[3]);
+        }
+    } else {
+        float *vzs = tb.vz + (size_t)cw * OT * C2_T;  // slot-major
+#pragma unroll
+        for (int j = 0; j < OT; ++j) vzs[j * C2_T + tid] = zr[j] * iph;
     }
 }
 
@@ -629,7 +649,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
     const float tau = (float)tv, inv_tau = (float)(C2_LOG2E / tv);  // log2 e / tau (c2_exp2)
     float *s = bf.s + (size_t)cw * tb.LM;
     constexpr int OTP = cw2_otp(OT);
-    const float *vz = tb.vz + (size_t)cw * OTP * C2_T;  // [512][OTP] thread-major
+    const float *vz = tb.vz + (size_t)cw * (cw2_vz_tm(OT) ? OTP : OT) * C2_T;  // [512][OTP] / [OT][512]
     // running statistics of sections tid and tid + 512 over this half's classes
     const int Lb = tb.Lblk;
     float Mr[2] = {-INFINITY, -INFINITY}, R1[2] = {0.f, 0.f}, R2[2] = {0.f, 0.f}, st[2] = {NAN, NAN};
@@ -680,7 +700,8 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
            // times the per-codeword bytes re-read from L2 every class.)
             constexpr int CH = OT > 12 ? (OT + 1) / 2 : OT;  // slots per load round (one round at 12 per thread)
             const __amdgpu_buffer_rsrc_t rg = c2_rsrc(tb.gf, 16 * OT * C2_T), rv = c2_rsrc(vz, 4 * OTP * C2_T),
-                                         rk = c2_rsrc(tb.kat, 4 * OTP * C2_T), rw = c2_rsrc(tb.wab, 8 * OT * C2_T);
+                                         rk = c2_rsrc(cw2_vz_tm(OT) ? tb.kat : tb.ka, 4 * OTP * C2_T),
+                                         rw = c2_rsrc(tb.wab, 8 * OT * C2_T);
             // one load round (CH == OT): a thread's slot words and z / phi in 16-byte loads (thread-major)
             uint32_t kall[CH == OT ? OT : 1], vall[CH == OT ? OT : 1];
             if constexpr (CH == OT) {
@@ -710,9 +731,10 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
                     if constexpr (CH == OT) {
                         ka[i] = kall[j];
                         vv[i] = __uint_as_float(vall[j]);
-                    } else {
-                        ka[i] = c2_ldu(rk, 4 * OTP * tl, 4 * j);
-                        vv[i] = c2_ldf(rv, 4 * OTP * tl, 4 * j);
+                    } else {  // (two load rounds: slot-major, each load a contiguous run of the wavefront --
+                              // thread-major, every lane of every per-slot load was a cache line of its own)
+                        ka[i] = c2_ldu(rk, 4 * tl, 4 * j * C2_T);
+                        vv[i] = c2_ldf(rv, 4 * tl, 4 * j * C2_T);
                     }
                     gc[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, 16 * tl, 16 * j * C2_T, 0));
                     if (!C2_ROWS_DERIVE)
