@@ -77,7 +77,7 @@ static_assert(C2_EPT == 16, "the transform is written for 16 values per thread")
 #endif
 // Ab: the accumulation's slot words requested after each transform (1) or at the class start (0) (A/B)
 #ifndef C2_AB_PF
-#define C2_AB_PF 0
+#define C2_AB_PF 1
 #endif
 #ifndef C2_STAGGER_SEL
 #define C2_STAGGER_SEL 0
@@ -434,9 +434,11 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
     // Software-pipelined over the classes: class m2's slice is requested, then the previous class's
     // transform (still in the image) is accumulated while the loads are in flight, then m2 is scattered
     // and transformed
-#if C2_AB_PF
-    uint32_t kapf[OT];
-#endif
+    // (at most 12 outputs per thread: the accumulation's slot words are class-invariant, so they are
+    // requested after each transform and arrive across the loop edge -- cw2_ab 0.397 -> 0.391 ms per launch,
+    // profiles/r05_c2_r13_fix.txt)
+    constexpr bool PF = C2_AB_PF && OT <= 12;
+    uint32_t kapf[PF ? OT : 1];
     for (int m2 = h * Qh; m2 < (h + 1) * Qh; ++m2) {
         const int tl = c2_opaque(tid);
         C2_TPC(0);
@@ -451,12 +453,10 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
             __syncthreads();
         }
         // (the accumulation's table loads first: vector-memory loads complete in order)
-#if C2_AB_PF
-        uint32_t (&ka)[OT] = kapf;
-#else
-        uint32_t ka[PL ? OT : 1];
-        if (PL && m2 > h * Qh) acc_tables(tl, ka);
-#endif
+        uint32_t kl[PL && !PF ? OT : 1];
+        if constexpr (PL && !PF)
+            if (m2 > h * Qh) acc_tables(tl, kl);
+        const uint32_t *ka = PF ? kapf : kl;
         float v[C2_SN];
         uint32_t e[C2_SN];
         {  // every load of the class slice in one round trip; past the class's end s reads 0 and the
@@ -501,9 +501,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
         C2_TPC(3);
         if (!C2_SKIP(1)) c2_fft<false>(tl, cmk);
         C2_TPC(6);
-#if C2_AB_PF
-        acc_tables(c2_opaque(tid), kapf);  // class-invariant: in flight across the loop edge
-#endif
+        if constexpr (PF) acc_tables(c2_opaque(tid), kapf);  // class-invariant: in flight across the loop edge
     }
     {
         uint32_t ka[OT];
