@@ -46,6 +46,8 @@ struct BlkTables {
     const uint32_t *pos2;     // [nT][8][1024] real LDS index (2 fsw(m) + component) of column entry
                               // j = tid + 1024 i, pairs (i = 2 i2, 2 i2 + 1) at [t][i2][tid]; the two-class
                               // engine: [nT][2][16][1024], 2 ppos(m1) + component per class (amp_block2.hip)
+    const uint32_t *pos1;     // two-class engine, one-table form (A/B, -DB2_ONETABLE=1): [nT][16][1024] per column
+                              // entry m1 << 2 | component << 1 | class (16 bits, pairs), both classes' passes
     const uint32_t *oab;      // [nT][Mr] (a mod 4096) | (b mod 4096) << 16 of output i
     const cx<float> *oc;      // [nT][Mr][8] X_i = Re(sum_r al_r Y[a mod 4096 + 4096 r] + be_r conj Y[b mod ...]),
                               // al_r = c1 w_N2^(r a), be_r = c2 conj w_N2^(r b) (the last FFT stage folded in)

@@ -104,6 +104,23 @@ __device__ __forceinline__ void b2_pos_load(const BlkTables &tb, int t, int m2, 
     for (int i = 0; i < B2_J / 2; ++i) pv[i] = p2[i * T + tid];
 }
 __device__ __forceinline__ uint32_t b2_pos(const uint32_t *pv, int i) { return (pv[i >> 1] >> (16 * (i & 1))) & 0xffffu; }
+// One-table form (A/B: -DB2_ONETABLE=1): one 16-bit entry per column entry and
+// transform for both classes, m1 << 2 | component << 1 | class, the padded index rebuilt per class pass --
+// half the position-table bytes, four vector instructions more per entry and pass
+#ifndef B2_ONETABLE
+#define B2_ONETABLE 0
+#endif
+template <int LP>
+__device__ __forceinline__ void b2_pos_load1(const BlkTables &tb, int t, int tid, uint32_t *pv) {
+    constexpr int T = B2G<LP>::THREADS;
+    const uint32_t *p1 = tb.pos1 + (size_t)t * (B2_J / 2) * T;
+#pragma unroll
+    for (int i = 0; i < B2_J / 2; ++i) pv[i] = p1[i * T + tid];
+}
+__device__ __forceinline__ uint32_t b2_pos1(const uint32_t *pv, int i, int m2) {
+    const uint32_t e = (pv[i >> 1] >> (16 * (i & 1))) & 0xffffu;
+    return (e & 1u) == (uint32_t)m2 ? 2u * (uint32_t)ppos((int)(e >> 2)) + ((e >> 1) & 1u) : (uint32_t)B2_TRASH;
+}
 
 // the first three stages (radix 16) of the P-point FFT over the padded image,
 // twiddles from the hardware sine / cosine (no table entries in flight: blk2_ab
@@ -136,11 +153,13 @@ __device__ __forceinline__ void b2_ab_column(const BlkTables &tb, const AmpBufs<
             const int tl = b2_opaque(tid);
             // the positions, in flight while the image clears
             uint32_t pv[B2_J / 2];
-            b2_pos_load<LP>(tb, t, m2, tl, pv);
+            if (B2_ONETABLE) b2_pos_load1<LP>(tb, t, tl, pv);
+            else b2_pos_load<LP>(tb, t, m2, tl, pv);
             b2_clear<LP>(smem, tl);
             __syncthreads();
 #pragma unroll
-            for (int i = 0; i < B2_J; ++i) dr[b2_pos(pv, i)] = bv[i];  // (the other class's entries: trash slot)
+            for (int i = 0; i < B2_J; ++i)  // (the other class's entries: trash slot)
+                dr[B2_ONETABLE ? b2_pos1(pv, i, m2) : b2_pos(pv, i)] = bv[i];
             // the output's bins and coefficients, requested before the transform (their L2 round trip
             // hides behind it; requested after it, one workgroup per CU waited for it every class)
             constexpr int RF = B2G<LP>::RF;
@@ -240,10 +259,11 @@ __global__ __launch_bounds__(B2G<LP>::THREADS, 4) void blk2_az(BlkTables tb, Amp
             // (stage twiddles from the hardware sine / cosine: no table entries in flight, u[] stays in registers)
             lds_fft1_sincos<true, 16, LP, 0, 4, true>(d, tl);
             uint32_t pv[B2_J / 2];
-            b2_pos_load<LP>(tb, t, m2, tl, pv);
+            if (B2_ONETABLE) b2_pos_load1<LP>(tb, t, tl, pv);
+            else b2_pos_load<LP>(tb, t, m2, tl, pv);
 #pragma unroll
-            for (int i = 0; i < B2_J; ++i) u[i] += dr[b2_pos(pv, i)];  // (the other class's entries read the
-                                                                      // zero trash slot)
+            for (int i = 0; i < B2_J; ++i)  // (the other class's entries read the zero trash slot)
+                u[i] += dr[B2_ONETABLE ? b2_pos1(pv, i, m2) : b2_pos(pv, i)];
             __syncthreads();
         }
     }

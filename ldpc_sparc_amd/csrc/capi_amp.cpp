@@ -91,7 +91,7 @@ struct sg_amp_plan {
     int b2_log2p = 0;            // classes of 2^13 points (two workgroups per CU); class size P = 2^b2_log2p
     int32_t *b_gk = nullptr;
     uint16_t *b_gloc = nullptr;
-    uint32_t *b_pos2 = nullptr, *b_oab = nullptr;
+    uint32_t *b_pos2 = nullptr, *b_pos1 = nullptr, *b_oab = nullptr;
     int32_t *b_gptr = nullptr, *b_gi = nullptr, *b_grow = nullptr;
     int b_ngs = 0;
     void *ws_gbuf = nullptr;  // [B][b_ngs] G slots (block engine)
@@ -294,7 +294,7 @@ static BlkTables btables(const sg_amp_plan *p) {
     tb.nT = p->nT; tb.L = p->L; tb.M = p->M; tb.LM = p->LM; tb.n = p->n; tb.Lr = p->Lr; tb.Lc = p->Lc;
     tb.Mr = p->Mr; tb.Mc = p->Mc;
     tb.col_ptr = p->col_ptr; tb.col_t = p->col_t; tb.t_row = p->t_row;
-    tb.pos2 = p->b_pos2; tb.oab = p->b_oab; tb.oc = (const cx<float> *)p->b_oc;
+    tb.pos2 = p->b_pos2; tb.pos1 = p->b_pos1; tb.oab = p->b_oab; tb.oc = (const cx<float> *)p->b_oc;
     tb.ngs = p->b_ngs; tb.gptr = p->b_gptr; tb.grow = p->b_grow; tb.gloc = p->b_gloc; tb.gi = p->b_gi; tb.gc = (const cx<float> *)p->b_gc;
     tb.gk = p->b_gk;
     tb.stw = (const cx<float> *)p->b_stw;
@@ -1123,6 +1123,7 @@ static int build_block2(sg_amp_plan *p, const uint32_t *order0, const uint32_t *
     constexpr uint32_t TRASH = 2 * 32;
     static_assert(ppos(32) == 33, "complex position 32 is a padding slot");
     std::vector<uint32_t> pos2((size_t)nT * 2 * (J / 2) * T, TRASH | (TRASH << 16));
+    std::vector<uint32_t> pos1((size_t)nT * (J / 2) * T, 0u);  // one-table form (amp_block2.hip B2_ONETABLE)
     std::vector<uint32_t> oab((size_t)nT * Mr);
     std::vector<cd> oc((size_t)nT * 2 * Mr * 8), gc;
     std::vector<int32_t> gptr(nT + 1, 0), gi, grow, gk;
@@ -1139,6 +1140,9 @@ static int build_block2(sg_amp_plan *p, const uint32_t *order0, const uint32_t *
             const int tid = (l / spw) * 64 + rr / eps, i = (l % spw) * eps + rr % eps;
             uint32_t &w = pos2[(((size_t)t * 2 + (m & 1)) * (J / 2) + i / 2) * T + tid];
             w = (w & ~(0xffffu << (16 * (i & 1)))) | (lds << (16 * (i & 1)));
+            const uint32_t e1 = (uint32_t)((m >> 1) << 2) | (uint32_t)((sl & 1) << 1) | (uint32_t)(m & 1);
+            SG_CHECK_ARG((m >> 1) < (1LL << 14), "internal: one-table entry beyond 16 bits");
+            pos1[((size_t)t * (J / 2) + i / 2) * T + tid] |= e1 << (16 * (i & 1));
         }
         std::vector<std::vector<std::pair<int, cd>>> gcon(N2);
         for (int i = 0; i < Mr; ++i) {
@@ -1182,6 +1186,7 @@ static int build_block2(sg_amp_plan *p, const uint32_t *order0, const uint32_t *
         }
     }
     SG_TRY(upload(p, &p->b_pos2, pos2));
+    SG_TRY(upload(p, &p->b_pos1, pos1));
     SG_TRY(upload(p, &p->b_oab, oab));
     SG_TRY(upload_cx(p, &p->b_oc, oc));
     SG_TRY(upload(p, &p->b_gptr, gptr));

@@ -1,6 +1,6 @@
 """C4: spatially coupled SPARC (omega=6, Lambda=32, L=1024, M=512, R=1.5,
 P=15, awgn_var=1, t_max=40; sparc_demo_sc_decode_wave) decoded on the GPU.
-args: B reps [R]"""
+args: B reps [R] [L]  (L = 2048: the notebook geometry, w = 2^16, the two-class block engine)"""
 import sys
 import time
 
@@ -12,7 +12,8 @@ from ldpc_sparc_amd import _native, sparc  # noqa: E402
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 R = float(sys.argv[3]) if len(sys.argv) > 3 else 1.5
-L, M, P, omega, Lam = 1024, 512, 15.0, 6, 32
+L = int(sys.argv[4]) if len(sys.argv) > 4 else 1024
+M, P, omega, Lam = 512, 15.0, 6, 32
 W = sparc.sc_basic(np.array(P), omega, Lam)
 Lr, Lc = W.shape
 n = int(round(L * 9 / R))
