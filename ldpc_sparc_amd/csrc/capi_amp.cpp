@@ -901,8 +901,10 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
     }
     // double precision: the split engine only (amp_cw2d.hip), its tables built directly; the plan then
     // counts as a per-codeword plan (use_cw), without the companion (f64 keeps P = 8192 either way)
+    // (the bounds of amp_cw2d.hip cw2d_launch_iter: its statistics launch takes a section's M <= 512 entries
+    // over Q <= 64 class segments in one wavefront, four sections per workgroup)
     if (p->precision == SG_F64 && nT == 1 && P == (1 << 13) && Lblk <= 2 * CW2_THREADS && p->L <= 1024 &&
-        Q % 2 == 0 && Q <= 70 && p->rmaxcls <= CW2_SLICE && !p->no_cw) {
+        p->L % 4 == 0 && M <= 512 && Q % 2 == 0 && Q <= 64 && p->rmaxcls <= CW2_SLICE && !p->no_cw) {
         SG_TRY(build_cw2(p, order0, t_scale[0], row_k1[0], cls_ptr, cls_ls));
         p->cw = p->cw2OT != 0;
     }

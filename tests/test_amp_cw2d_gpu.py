@@ -100,3 +100,13 @@ def test_f64_shipped_choice_full_batch(monkeypatch):
     assert np.array_equal(ta, tb)
     assert np.array_equal(ma, mb)
     np.testing.assert_allclose(na, nb, rtol=0, atol=1e-9)
+
+
+def test_f64_outside_split_engine_bounds_takes_staged(monkeypatch):
+    """A design outside the f64 split engine's bounds (M = 1024 > 512 entries per section for its
+    one-wavefront statistics) at a batch that fills the CUs: the plan keeps the staged engine, and the
+    decode runs (no SG_ERR_UNSUPPORTED at decode time)."""
+    op, true, Y = _batch(256, 1024, 1.5, 256, 3, 4)
+    (m, t, nm, _), info = _decode(monkeypatch, op, Y, true, None, t_max=6)
+    assert info["engine"] == 1
+    assert np.all(t >= 1) and np.isfinite(nm).all()
