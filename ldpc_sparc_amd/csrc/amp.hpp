@@ -209,6 +209,9 @@ __host__ __device__ constexpr int c2pos(int i) { return i + (i >> 5); }
 constexpr uint32_t CW2_TRASH = 2 * (8192 + 256) + 2048;  // LDS float index of the trash slot (after the
                                                          // padded image and the statistics)
 constexpr uint32_t CW_SELF = 1u << 23;  // the pair's two rows coincide (r = 0 or P / 2)
+// bits 24-26 of a split-engine slot word (f32): the output's phase offset o in units of N / 2 (build_cw2
+// polar form: al = |al| e^(2 pi i (3a + o N/2) / 4N), be = |be| e^(2 pi i (N - 3a - o N/2) / 4N))
+constexpr int CW_OFFSHIFT = 24;
 // a thread's slots padded to a multiple of four (thread-major tables: 16-byte loads)
 __host__ __device__ constexpr int cw2_otp(int ot) { return (ot + 3) & ~3; }
 // z / phi thread-major (one load round of 16-byte loads in cw2_az) up to 12 slots per thread; above, cw2_az
@@ -223,17 +226,22 @@ struct Cw2Tables {
     const int32_t *oi;        // [OT][512] output index (invalid slots: 0)
     const float4 *cf;         // [OT][512] (c1, c2): output = Re(c1 H[a] + c2 conj H[N2 - a])
     const float4 *gf;         // [OT][512] (al, be): G[a] += al z/phi, G[N2 - a] += be z/phi
+    const float2 *gm;         // [OT][512] (|al|, |be|) of the polar form (CW_OFFSHIFT; cw2_ctrl scales z/phi)
+    int sh_off;               // log2(N / 2): the slot's phase offset o N/2 = o << sh_off
+    uint32_t m4n;             // 4N - 1 (phases in units of 1 / 4N revolutions, N = 2 N2 a power of two)
+    float inv_4n;             // 1 / 4N
     const int32_t *cls_ptr;   // [Q+1]
     const uint32_t *cls_ls;   // [Mc] padded real LDS index | section << 16
     const uint32_t *cls2;     // [Q][9216] cls_ls of each class padded to 9216 entries with CW2_TRASH
+    const uint32_t *clsp;     // [Q][4608] image positions of entries q and q + 4608 of cls2 (low, high half)
     const int32_t *qpos;      // [Mc]
     const uint16_t *seg;      // [Q][Lblk+1]
     float *xr;                // [B][2][OT][512] each half's part of Re(c1 H[a] + c2 conj H[b]) per output
     const uint2 *rab;         // [OT][512] LDS byte addresses of rows r, P - r of the slot's output (cw2_ab reads)
     const uint2 *wab;         // [OT][512] LDS byte addresses of the slot's row writes (rows r, P - r on the
                               // pair's last slot, else the trash slot; r = 0, P / 2: row r and trash)
-    float *vz;                // z / phi in slot order: [B][512][OTP] thread-major (OTP = OT rounded up to 4) if
-                              // cw2_vz_tm(OT), else [B][OT][512]
+    float *vz;                // z / phi in slot order, times (|al|, |be|) (two floats per slot): [B][512][OTP][2]
+                              // thread-major (OTP = OT rounded up to 4) if cw2_vz_tm(OT), else [B][OT][512][2]
     float *ys, *zs;           // [B][OT][512] y (copied at t = 0) and z in slot order (cw2_ctrl reads them
                               // coalesced; z in natural order is still written for a hand-over)
     float4 *part;             // [B][2][Lblk] partial section statistics (max, R1, R2, s of the true entry or NaN)

@@ -75,6 +75,15 @@ static_assert(C2_EPT == 16, "the transform is written for 16 values per thread")
 #ifndef C2_ROWS_DERIVE
 #define C2_ROWS_DERIVE 1
 #endif
+// Az rows in the polar form (build_cw2): one phase per slot and class from the slot word, z/phi scaled by
+// (|al|, |be|) -- no per-slot complex coefficient table (gf) re-read every class (1), or that table (0) (A/B)
+#ifndef C2_POLAR
+#define C2_POLAR 1
+#endif
+// Az: the gathers' image positions from the packed 16-bit table clsp (1) or the full class words cls2 (0) (A/B)
+#ifndef C2_AZPOS
+#define C2_AZPOS 1
+#endif
 // Ab: the accumulation's slot words requested after each transform (1) or at the class start (0) (A/B)
 #ifndef C2_AB_PF
 #define C2_AB_PF 1
@@ -561,6 +570,7 @@ __global__ __launch_bounds__(C2_T) void cw2_ctrl(Cw2Tables tb, RegBufs<float> bf
     }
     const float *xr0 = tb.xr + (size_t)cw * 2 * OT * C2_T, *xr1 = xr0 + (size_t)OT * C2_T;
     float zr[OT];
+    float2 gmv[C2_POLAR ? OT : 1];
     double acc = 0.0;
     {
         // every load first, in one round trip (the uniform branch outside the slot loops: written per slot,
@@ -574,6 +584,7 @@ __global__ __launch_bounds__(C2_T) void cw2_ctrl(Cw2Tables tb, RegBufs<float> bf
         for (int j = 0; j < OT; ++j) {
             oi[j] = tb.oi[j * C2_T + tid];
             kv[j] = tb.ka[j * C2_T + tid];
+            if constexpr (C2_POLAR != 0) gmv[j] = tb.gm[j * C2_T + tid];
         }
         if (have_beta) {  // y, the previous z and the two halves' parts in slot order: coalesced
 #pragma unroll
@@ -617,6 +628,32 @@ __global__ __launch_bounds__(C2_T) void cw2_ctrl(Cw2Tables tb, RegBufs<float> bf
     }
     const float iph = (float)(1.0 / phi);
     constexpr int OTP = cw2_otp(OT);
+#if C2_POLAR
+    // z / phi times the slot's (|al|, |be|) (build_cw2 polar form), two floats per slot; padding slots 0
+    if constexpr (cw2_vz_tm(OT)) {
+        float4 *vz4 = reinterpret_cast<float4 *>(tb.vz + ((size_t)cw * C2_T + tid) * OTP * 2);  // thread-major
+#pragma unroll
+        for (int q = 0; q < OTP / 2; ++q) {
+            float w[4];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const int j = 2 * q + c;
+                const float2 g = j < OT ? gmv[j] : make_float2(0.f, 0.f);
+                const float v = j < OT ? zr[j] * iph : 0.f;
+                w[2 * c] = v * g.x;
+                w[2 * c + 1] = v * g.y;
+            }
+            vz4[q] = make_float4(w[0], w[1], w[2], w[3]);
+        }
+    } else {
+        float2 *vzs = reinterpret_cast<float2 *>(tb.vz) + (size_t)cw * OT * C2_T;  // slot-major
+#pragma unroll
+        for (int j = 0; j < OT; ++j) {
+            const float v = zr[j] * iph;
+            vzs[j * C2_T + tid] = make_float2(v * gmv[j].x, v * gmv[j].y);
+        }
+    }
+#else
     if constexpr (cw2_vz_tm(OT)) {
         float4 *vz4 = reinterpret_cast<float4 *>(tb.vz + ((size_t)cw * C2_T + tid) * OTP);  // thread-major
 #pragma unroll
@@ -631,6 +668,7 @@ __global__ __launch_bounds__(C2_T) void cw2_ctrl(Cw2Tables tb, RegBufs<float> bf
 #pragma unroll
         for (int j = 0; j < OT; ++j) vzs[j * C2_T + tid] = zr[j] * iph;
     }
+#endif
 }
 
 // ---------------------------------------------------------------------------- Az
@@ -647,7 +685,8 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
     const float tau = (float)tv, inv_tau = (float)(C2_LOG2E / tv);  // log2 e / tau (c2_exp2)
     float *s = bf.s + (size_t)cw * tb.LM;
     constexpr int OTP = cw2_otp(OT);
-    const float *vz = tb.vz + (size_t)cw * (cw2_vz_tm(OT) ? OTP : OT) * C2_T;  // [512][OTP] / [OT][512]
+    // [512][OTP][2] / [OT][512][2] (polar form: (|al|, |be|) z / phi); [512][OTP] / [OT][512] (C2_POLAR 0)
+    const float *vz = tb.vz + (size_t)cw * (cw2_vz_tm(OT) ? OTP : OT) * C2_T * (C2_POLAR ? 2 : 1);
     // running statistics of sections tid and tid + 512 over this half's classes
     const int Lb = tb.Lblk;
     float Mr[2] = {-INFINITY, -INFINITY}, R1[2] = {0.f, 0.f}, R2[2] = {0.f, 0.f}, st[2] = {NAN, NAN};
@@ -677,7 +716,21 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
         float v[C2_SN];
         uint32_t e[C2_SN];
         auto load_slice = [&]() {
+#if C2_AZPOS
+            // the entries' image positions two per word (clsp: entries i and i + 9 of the thread), half the
+            // table loads and bytes of the full words (the sections are not needed here)
+            const __amdgpu_buffer_rsrc_t re = c2_rsrc(tb.clsp + (size_t)m2 * (CW2_SLICE / 2), 2 * CW2_SLICE);
+#pragma unroll
+            for (int i = 0; i < C2_SN / 2; ++i) {
+                const uint32_t w = c2_ldu(re, 4 * tl, 4 * i * C2_T);
+                e[i] = w & 0xffffu;
+                e[i + C2_SN / 2] = w >> 16;
+            }
+#else
             const __amdgpu_buffer_rsrc_t re = c2_rsrc(tb.cls2 + (size_t)m2 * CW2_SLICE, 4 * CW2_SLICE);
+#pragma unroll
+            for (int i = 0; i < C2_SN; ++i) e[i] = c2_ldu(re, 4 * tl, 4 * i * C2_T);
+#endif
 #pragma unroll
             for (int i = 0; i < C2_SN; ++i) {
                 if (C2_SKIP(128)) {  // (synthetic entries inside the image, section 0)
@@ -685,10 +738,81 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
                     e[i] = (uint32_t)(((tl * 37 + i * 4099) & 8191) * 2);
                     continue;
                 }
-                e[i] = c2_ldu(re, 4 * tl, 4 * i * C2_T);
                 v[i] = c2_ldf(rs, 4 * tl + 4 * i * C2_T, 0);  // (t = 0: unused)
             }
         };
+#if C2_POLAR
+        if (!C2_SKIP(16)) {  // rows r and P - r of each owned pair: sum of al v conj(W) / be v W over its outputs
+            // (v = z / phi).  Polar form (build_cw2): al conj(W) = |al| (cos x, sin x) and be W = |be| (sin x,
+            // cos x) with x = ((3 + 8 m2) a + o N/2) / 4N revolutions from the slot word alone, and cw2_ctrl
+            // stores (|al| v, |be| v): per slot and class one phase, two packed FMAs per row, and 12 bytes of
+            // tables instead of 24 (the complex al, be were 16 of them).  Branch-free: every slot accumulates
+            // (NEWROW restarts the sums) and writes both rows -- the pair's rows on its last slot (ENDROW), the
+            // trash slot otherwise (invalid slots: zero scale) -- so the two pairs whose rows coincide (r = 0,
+            // P / 2) write their sum.  (Slot words and v reloaded per class from L1 / L2: held across the
+            // transform, or loaded one class ahead, they spill.)
+            constexpr int CH = OT > 12 ? (OT + 1) / 2 : OT;  // slots per load round (one round at 12 per thread)
+            const __amdgpu_buffer_rsrc_t rv = c2_rsrc(vz, 8 * OTP * C2_T),
+                                         rk = c2_rsrc(cw2_vz_tm(OT) ? tb.kat : tb.ka, 4 * OTP * C2_T);
+            uint32_t kall[CH == OT ? OT : 1];
+            c2f vall[CH == OT ? OT : 1];
+            if constexpr (CH == OT) {  // one load round: a thread's slot words and scaled z / phi, 16-byte loads
+                if (!C2_SKIP(32)) {
+                    c2_ld_slots<OT>(rk, tl, kall);
+#pragma unroll
+                    for (int q = 0; q < OTP / 2; ++q) {
+                        const auto w = __builtin_amdgcn_raw_buffer_load_b128(rv, 8 * OTP * tl, 16 * q, 0);
+                        if (2 * q < OT) vall[2 * q] = c2f{__uint_as_float(w[0]), __uint_as_float(w[1])};
+                        if (2 * q + 1 < OT) vall[2 * q + 1] = c2f{__uint_as_float(w[2]), __uint_as_float(w[3])};
+                    }
+                }
+            }
+            const uint32_t cm = 3u + 8u * (uint32_t)m2;
+            c2f u0{0.f, 0.f}, u1{0.f, 0.f};
+#pragma unroll
+            for (int j0 = 0; j0 < OT; j0 += CH) {
+                uint32_t ka[CH];
+                c2f vv[CH];
+#pragma unroll
+                for (int i = 0; i < CH; ++i) {
+                    const int j = j0 + i < OT ? j0 + i : OT - 1;
+                    if (C2_SKIP(32)) {
+                        const uint32_t r = (uint32_t)(tl * 8 + j) & 4095u;
+                        ka[i] = r | CW_VALID | ((j & 1) ? CW_ENDROW : CW_NEWROW);
+                        vv[i] = c2f{0.5f, (float)j};
+                        continue;
+                    }
+                    if constexpr (CH == OT) {
+                        ka[i] = kall[j];
+                        vv[i] = vall[j];
+                    } else {  // (two load rounds: slot-major, each load a contiguous run of the wavefront)
+                        ka[i] = c2_ldu(rk, 4 * tl, 4 * j * C2_T);
+                        const auto w = __builtin_amdgcn_raw_buffer_load_b64(rv, 8 * tl, 8 * j * C2_T, 0);
+                        vv[i] = c2f{__uint_as_float(w[0]), __uint_as_float(w[1])};
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < CH; ++j) {
+                    if (j0 + j >= OT) break;
+                    const uint32_t k = ka[j];
+                    const uint32_t xu =
+                        (__umul24(cm, k & CW_KMASK) + (((k >> CW_OFFSHIFT) & 7u) << tb.sh_off)) & tb.m4n;
+                    const float x = (float)xu * tb.inv_4n;  // (exact: 4N <= 2^24)
+                    const c2f cs = c2f{__builtin_amdgcn_cosf(x), __builtin_amdgcn_sinf(x)};
+                    const float keep = (k & CW_NEWROW) ? 0.f : 1.f;
+                    u0 = __builtin_elementwise_fma(cs, vv[j].xx, u0 * keep);
+                    u1 = __builtin_elementwise_fma(cs.yx, vv[j].yy, u1 * keep);
+                    const int r = (int)(k & (uint32_t)(C2_P - 1)), rb = C2_P - r;
+                    const bool end = (k & CW_ENDROW) != 0;
+                    c2lds *pa = (c2lds *)(size_t)(end ? 8u * (uint32_t)c2pos(r) : 4u * CW2_TRASH);
+                    c2lds *pb = (c2lds *)(size_t)((end && !(k & CW_SELF)) ? 8u * (uint32_t)c2pos(rb) : 4u * CW2_TRASH);
+                    *pa = u0;
+                    *pb = u1;
+                    if (k & CW_SELF) *pa = u0 + u1;
+                }
+            }
+        }
+#else
         if (!C2_SKIP(16)) {  // rows r and P - r of each owned pair: sum of al v conj(W) / be v W over its outputs (v = z / phi),
            // branch-free: every slot accumulates (NEWROW restarts the sums) and writes both rows -- the
            // pair's rows on its last slot (ENDROW), the trash slot otherwise (invalid slots: al = be = 0),
@@ -759,6 +883,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
                 }
             }
         }
+#endif
         // (requested after the rows' table loads: vector-memory loads complete in order, so a slice
         // requested before them would hold the rows up for its whole HBM latency)
         if constexpr (EARLY) load_slice();
@@ -784,7 +909,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
 #pragma unroll
             for (int i = 0; i < C2_SN; ++i) {  // s = beta_prev + tau u (sparc.py:972); beta_prev stored by cw2_ab
                 const float b = have_beta ? v[i] : 0.f;
-                snv[i] = b + tau * (C2_SKIP(1024) ? (float)i : dr[e[i] & 0xffffu]);
+                snv[i] = b + tau * (C2_SKIP(1024) ? (float)i : dr[C2_AZPOS ? e[i] : e[i] & 0xffffu]);
             }
         }
         C2_TPC(36);

@@ -74,10 +74,12 @@ struct sg_amp_plan {
     uint32_t *c_kt = nullptr;
     // split per-codeword engine (amp_cw2.hip): outputs per thread (0 = not built) and its tables
     int cw2OT = 0;
-    uint32_t *c2_ka = nullptr, *c2_kat = nullptr, *c2_cmask = nullptr, *c2_cls = nullptr;
+    uint32_t *c2_ka = nullptr, *c2_kat = nullptr, *c2_cmask = nullptr, *c2_cls = nullptr, *c2_clsp = nullptr;
     int32_t *c2_oi = nullptr;
     uint32_t *c2_wab = nullptr, *c2_rab = nullptr;
     void *c2_cf = nullptr, *c2_gf = nullptr;
+    float *c2_gm = nullptr;  // [OT][512][2] (|al|, |be|) of the polar row form (build_cw2)
+    int c2_shoff = 0;        // log2(N / 2): unit of the slot's phase offset
     // its double-precision form (amp_cw2d.hip): coefficients, the slots' w_N2^a, the P-point twiddles
     double *c2d_cf = nullptr, *c2d_gf = nullptr, *c2d_sa = nullptr, *c2d_twp = nullptr;
     void *ws_c2xp = nullptr, *ws_c2vz = nullptr, *ws_c2part = nullptr, *ws_c2ys = nullptr, *ws_c2zs = nullptr;
@@ -223,7 +225,7 @@ static int ensure_ws(sg_amp_plan *p, int B, int t_max) {
         }
         if (p->cw2OT) {  // (reals of the plan's precision; partial statistics: four per section)
             SG_ALLOC(p->ws_c2xp, Bz * 2 * p->cw2OT * CW2_THREADS * rs);
-            SG_ALLOC(p->ws_c2vz, Bz * cw2_otp(p->cw2OT) * CW2_THREADS * rs);
+            SG_ALLOC(p->ws_c2vz, Bz * cw2_otp(p->cw2OT) * CW2_THREADS * 8);  // (f32: two reals per slot)
             SG_ALLOC(p->ws_c2ys, Bz * p->cw2OT * CW2_THREADS * rs);
             SG_ALLOC(p->ws_c2zs, Bz * p->cw2OT * CW2_THREADS * rs);
             SG_ALLOC(p->ws_c2part, Bz * 2 * p->Lblk * 4 * rs);
@@ -564,6 +566,34 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
         sad(f64 ? (size_t)OT * T * 2 : 0, 0.0);
     for (size_t i = 0; i < sad.size(); i += 2) sad[i] = 1.0;  // invalid slots: S = 1
     std::vector<uint32_t> wab((size_t)OT * T * 2, 4u * CW2_TRASH), rab((size_t)OT * T * 2, 0u);
+    // Polar form of the inverse coefficients (amp_cw2.hip Az rows): with U = 1 / (4N) revolutions,
+    // inv_contrib's al and be are real multiples of unit phasors, al = |al| e^(2 pi i A U) and
+    // be = |be| e^(2 pi i (N - A) U), A = 3a + o N/2 (o in {0, 1, 6, 7} by the output's case: q below or
+    // above N2, normalised by a swap or not).  Then the rows' al conj(W) and be W (W = w_N2^(m2 a)) are
+    // |al| (cos x, sin x) and |be| (sin x, cos x) of ONE angle x = ((3 + 8 m2) a + o N/2) U: the rows
+    // need the slot word and z/phi scaled by |al|, |be| (cw2_ctrl), not the complex (al, be) per class.
+    // Fitted and checked per output here (any mismatch: no split engine for the plan).
+    std::vector<float> gm((size_t)OT * T * 2, 0.f);
+    const bool pow2 = N >= 4 && (N & (N - 1)) == 0 && 4 * N <= (1ll << 24);
+    auto polar = [&](const Out &o, uint32_t *code, double *ma, double *mb) -> bool {
+        if (!pow2) return false;
+        const long long N4 = 4 * N;
+        double best = 1e300;
+        for (uint32_t c : {0u, 1u, 6u, 7u}) {
+            const long long A = ((3 * o.a + (long long)c * (N / 2)) % N4 + N4) % N4;
+            const cd ra = o.al * expi(-2.0 * M_PI * (double)A / (double)N4);
+            const cd rb = o.be * expi(-2.0 * M_PI * (double)(N - A) / (double)N4);
+            const double err = std::abs(ra.imag()) + std::abs(rb.imag());
+            if (err < best) {
+                best = err;
+                *code = c;
+                *ma = ra.real();
+                *mb = rb.real();
+            }
+        }
+        return best <= 1e-12 * (std::abs(o.al) + std::abs(o.be) + 1e-300);
+    };
+    if (p->precision != SG_F64 && !pow2) return SG_OK;
     for (int tid = 0; tid < T; ++tid) {
         int j = 0;
         for (int r : own[tid]) {
@@ -576,6 +606,14 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
                 if (q + 1 == lst.size()) e |= CW_ENDROW;
                 if (r == 0 || 2 * r == P) e |= CW_SELF;
                 const size_t c = (size_t)j * T + tid;
+                if (p->precision != SG_F64) {
+                    uint32_t code = 0;
+                    double ma = 0.0, mb = 0.0;
+                    if (!polar(o, &code, &ma, &mb)) return SG_OK;  // (not the DCT's coefficients: no split engine)
+                    e |= code << CW_OFFSHIFT;
+                    gm[2 * c] = (float)ma;
+                    gm[2 * c + 1] = (float)mb;
+                }
                 ka[c] = e;
                 rab[2 * c] = 8u * (uint32_t)c2pos(r);
                 rab[2 * c + 1] = 8u * (uint32_t)c2pos((P - r) % P);
@@ -631,6 +669,16 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
             cls2[(size_t)m2 * CW2_SLICE + (q - cls_ptr[m2])] = (cls_ls[q] & ~0xffffu) | pl;
         }
     SG_TRY(upload(p, &p->c2_cls, cls2));
+    {  // image positions alone, two per word (cw2_az's gathers: entries tl + 512 i and tl + 512 (i + 9))
+        constexpr int H = CW2_SLICE / 2;
+        std::vector<uint32_t> clsp((size_t)Q * H);
+        for (int m2 = 0; m2 < Q; ++m2)
+            for (int q = 0; q < H; ++q) {
+                const uint32_t *c = &cls2[(size_t)m2 * CW2_SLICE];
+                clsp[(size_t)m2 * H + q] = (c[q] & 0xffffu) | (c[q + H] << 16);
+            }
+        SG_TRY(upload(p, &p->c2_clsp, clsp));
+    }
     SG_TRY(upload(p, &p->c2_cmask, cmask));
     SG_TRY(upload(p, &p->c2_ka, ka));
     {  // thread-major copy: thread tid's slots at [tid][OTP] (amp_cw2.hip loads them 16 bytes at a time)
@@ -648,6 +696,8 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
     SG_TRY(upload(p, &dgf, gf));
     p->c2_cf = dcf;
     p->c2_gf = dgf;
+    SG_TRY(upload(p, &p->c2_gm, gm));
+    p->c2_shoff = pow2 ? ilog2((int)(N / 2)) : 0;
     if (f64) {
         std::vector<double> twp((size_t)P * 2);
         for (int k = 0; k < P; ++k) {
@@ -956,8 +1006,9 @@ static Cw2Tables c2tables(const sg_amp_plan *p, int B) {
     tb.OT = p->cw2OT; tb.maxcls = p->rmaxcls;
     tb.inv_n2 = 1.0f / (float)p->N2;
     tb.cmask = p->c2_cmask; tb.ka = p->c2_ka; tb.kat = p->c2_kat; tb.oi = p->c2_oi;
-    tb.cf = (const float4 *)p->c2_cf; tb.gf = (const float4 *)p->c2_gf;
-    tb.cls_ptr = p->r_cls_ptr; tb.cls_ls = p->r_cls_ls; tb.cls2 = p->c2_cls; tb.qpos = p->r_qpos; tb.seg = p->r_seg;
+    tb.cf = (const float4 *)p->c2_cf; tb.gf = (const float4 *)p->c2_gf; tb.gm = (const float2 *)p->c2_gm;
+    tb.sh_off = p->c2_shoff; tb.m4n = (uint32_t)(4 * p->w - 1); tb.inv_4n = (float)(1.0 / (4.0 * (double)p->w));
+    tb.cls_ptr = p->r_cls_ptr; tb.cls_ls = p->r_cls_ls; tb.cls2 = p->c2_cls; tb.clsp = p->c2_clsp; tb.qpos = p->r_qpos; tb.seg = p->r_seg;
     tb.xr = (float *)p->ws_c2xp; tb.vz = (float *)p->ws_c2vz; tb.ys = (float *)p->ws_c2ys; tb.zs = (float *)p->ws_c2zs; tb.wab = (const uint2 *)p->c2_wab; tb.rab = (const uint2 *)p->c2_rab; tb.part = (float4 *)p->ws_c2part;
     // [2 B][64] stamps, only when the diagnostics buffer holds them (build_cw2
     // accepts any even Q, and B * Q * 20 < 128 B for Q < 7)
