@@ -84,6 +84,24 @@ static_assert(C2_EPT == 16, "the transform is written for 16 values per thread")
 #ifndef C2_AZPOS
 #define C2_AZPOS 1
 #endif
+// Wave issue priority during the transforms and outside them.  Two workgroups share a CU and alternate
+// between the transform (VALU and LDS throughput) and phases that are chains of memory round trips and
+// barriers (class loads, rows, gathers, statistics).  At equal priority the older wave wins each issue
+// slot, so a workgroup's chain waited behind the other's transform; with the chains at 1 over the
+// transforms at 0 the transform fills the chains' gaps instead: cw2_az 0.531 -> 0.501, cw2_ab 0.382 ->
+// 0.378 ms per launch, C2 probe 11.77 k -> 12.29 k codewords/s same box, identical results (priority 2 or
+// 3 for the chains, 2 for the statistics alone, or Az alone measured the same or less:
+// profiles/r05_prio_ab.txt).  Both 0: flat, for the A/B.
+#ifndef C2_PRIO_FFT
+#define C2_PRIO_FFT 0
+#endif
+#ifndef C2_PRIO_REST
+#define C2_PRIO_REST 1
+#endif
+#define C2_SETPRIO(p)                                                       \
+    do {                                                                    \
+        if (C2_PRIO_FFT != 0 || C2_PRIO_REST != 0) __builtin_amdgcn_s_setprio(p); \
+    } while (0)
 // Ab: the accumulation's slot words requested after each transform (1) or at the class start (0) (A/B)
 #ifndef C2_AB_PF
 #define C2_AB_PF 1
@@ -405,6 +423,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
     const int h = blockIdx.x & 1, cw = blockIdx.x >> 1, tid = threadIdx.x;
     if (!bf.active[cw]) return;
     c2_stagger();
+    C2_SETPRIO(C2_PRIO_REST);
     const size_t lb = (size_t)cw * tb.L;
     for (int l = tid; l < tb.L; l += C2_T) {  // previous beta's section max, 1/sum
         sMI[l] = c2f{bf.stM[lb + l], bf.stI[lb + l]};
@@ -508,7 +527,9 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
         }
         __syncthreads();
         C2_TPC(3);
+        C2_SETPRIO(C2_PRIO_FFT);
         if (!C2_SKIP(1)) c2_fft<false>(tl, cmk);
+        C2_SETPRIO(C2_PRIO_REST);
         C2_TPC(6);
         if constexpr (PF) acc_tables(c2_opaque(tid), kapf);  // class-invariant: in flight across the loop edge
     }
@@ -679,6 +700,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
     const int h = blockIdx.x & 1, cw = blockIdx.x >> 1, tid = threadIdx.x;
     if (!bf.active[cw]) return;
     c2_stagger();
+    C2_SETPRIO(C2_PRIO_REST);
     const size_t lb = (size_t)cw * tb.L;
     const bool have_beta = t > 0;
     const double tv = bf.tau[cw];
@@ -901,7 +923,9 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
         C2_TPC(33);
         __syncthreads();
         C2_TPC(34);
+        C2_SETPRIO(C2_PRIO_FFT);
         if (!C2_SKIP(8)) c2_fft<true>(tl, rmk);
+        C2_SETPRIO(C2_PRIO_REST);
         C2_TPC(35);
         float snv[C2_SN];
         if constexpr (!EARLY) load_slice();

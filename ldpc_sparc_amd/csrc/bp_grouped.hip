@@ -44,6 +44,17 @@ constexpr float GRP_CH_MAX = 1e30f;
 #ifndef BPG_CHECK_PAIRS
 #define BPG_CHECK_PAIRS 0
 #endif
+// Wave issue priority of the variable and the check pass.  Four workgroups share a CU, each pass a chain
+// of table / LDS round trips between two barriers; the check pass at 1 over the variable pass at 0:
+// 0.694 / 0.701 / 0.685 -> 0.659 / 0.661 / 0.654 ms per launch at 1.0 / 1.5 / 2.0 dB, same box, bit-identical
+// (check pass at 2 or 3, or variable pass at 1 under a check pass at 2, within noise of it:
+// profiles/r05_prio_ab.txt).  Both equal: flat, for the A/B.
+#ifndef BPG_PRIO_V
+#define BPG_PRIO_V 0
+#endif
+#ifndef BPG_PRIO_C
+#define BPG_PRIO_C 1
+#endif
 #ifndef BPG_SETUP_BATCH
 #define BPG_SETUP_BATCH 0
 #endif
@@ -349,7 +360,9 @@ __global__ __launch_bounds__(BP_THREADS, VJ <= 4 ? 8 : 6) void bp_grouped_minsum
         // ended it)
         int it = 0;
         for (; it < a.max_it; ++it) {
+            if (BPG_PRIO_V != BPG_PRIO_C) __builtin_amdgcn_s_setprio(BPG_PRIO_V);
             var_pass(it == 0);  // (the first: zero incoming messages, no reads, no zeroed image)
+            if (BPG_PRIO_V != BPG_PRIO_C) __builtin_amdgcn_s_setprio(BPG_PRIO_C);
             __syncthreads();
             // ---- check pass (c_ldpc.c:183-194 with the min-sum update)
             uint32_t unsat = 0u;

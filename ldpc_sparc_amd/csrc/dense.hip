@@ -52,6 +52,15 @@ __device__ __forceinline__ float4 gemm_ld_y(const float *p) {
 }
 template <int MT>
 constexpr int gbm() { return 64 * MT; }
+// Issue priority of a wave's MFMA loop (0: flat, for the A/B).  Two workgroups share a CU, so each SIMD
+// runs one wave of each; at equal priority the older wave wins the issue arbitration, and a wave in its
+// staging phase (LDS stores, barriers, next loads) held the MFMA pipe of the other one back.  The MFMA
+// loop at 1 over a staging phase at 0: 18.88 -> 18.24 ms per C5 GEMM launch (0.833 -> 0.862 of the f32
+// MFMA peak) same box, bit-identical; 2 and 3 measure the same (profiles/r05_prio_ab.txt).  Without the
+// staging phase at all (barriers and LDS stores dropped, garbage results) the loop runs at 0.96.
+#ifndef GEMM_PRIO
+#define GEMM_PRIO 1
+#endif
 
 template <bool NT, int MT>
 __global__ __launch_bounds__(256, MT == 4 ? 2 : 1) void gemm_f32_mfma(GemmF32 g) {  // (MT 4: 2 waves per SIMD)
@@ -99,6 +108,7 @@ __global__ __launch_bounds__(256, MT == 4 ? 2 : 1) void gemm_f32_mfma(GemmF32 g)
             for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
     if (nk > 0) load(kb);
     for (int kt = 0; kt < nk; ++kt) {
+        if (GEMM_PRIO) __builtin_amdgcn_s_setprio(0);
         __syncthreads();
 #pragma unroll
         for (int p = 0; p < XL; ++p) {
@@ -121,6 +131,7 @@ __global__ __launch_bounds__(256, MT == 4 ? 2 : 1) void gemm_f32_mfma(GemmF32 g)
         }
         __syncthreads();
         if (kt + 1 < nk) load(kb + (kt + 1) * GBK);  // next tile in flight during the MFMAs
+        if (GEMM_PRIO) __builtin_amdgcn_s_setprio(GEMM_PRIO);
 #pragma unroll
         for (int kk = 0; kk < GBK / 2; ++kk) {
             const int kx = 2 * kk + (lane >> 5);
