@@ -107,14 +107,17 @@ __device__ __forceinline__ uint32_t b2_pos(const uint32_t *pv, int i) { return (
 // One-table form (A/B: -DB2_ONETABLE=1): one 16-bit entry per column entry and
 // transform for both classes, m1 << 2 | component << 1 | class, the padded index rebuilt per class pass --
 // half the position-table bytes, four vector instructions more per entry and pass
-// Wave issue priority: the transforms at 0, everything else (class scatters and gathers, rows, the
-// sections) at 1, as in the split C2 engine (amp_cw2.hip); two workgroups share a CU at LP = 13
-#ifndef B2_PRIO
-#define B2_PRIO 1
+// Wave issue priority of the transforms and of the rest (A/B; flat by default: the split C2 engine's
+// scheme -- transforms 0, the rest 1 -- measured 1000 -> 945 codewords/s here, profiles/r05_prio_ab.txt)
+#ifndef B2_PRIO_FFT
+#define B2_PRIO_FFT 0
 #endif
-#define B2_SETPRIO(p)                                        \
-    do {                                                     \
-        if (B2_PRIO) __builtin_amdgcn_s_setprio(p);          \
+#ifndef B2_PRIO_REST
+#define B2_PRIO_REST 0
+#endif
+#define B2_SETPRIO(p)                                                       \
+    do {                                                                    \
+        if (B2_PRIO_FFT != B2_PRIO_REST) __builtin_amdgcn_s_setprio(p);     \
     } while (0)
 #ifndef B2_ONETABLE
 #define B2_ONETABLE 0
@@ -183,9 +186,9 @@ __device__ __forceinline__ void b2_ab_column(const BlkTables &tb, const AmpBufs<
                 be[r] = oc[4 + r];
             }
             __syncthreads();
-            B2_SETPRIO(0);
+            B2_SETPRIO(B2_PRIO_FFT);
             b2_fwd_stages<LP>(d, tl);
-            B2_SETPRIO(1);
+            B2_SETPRIO(B2_PRIO_REST);
             // X_i += Re(sum_r al_r Y[a mod 4096 + 4096 r] + be_r conj Y[b mod ...]), r < RF:
             // the last stage and w_N2^(m2 k) are in the coefficients
             if (own) {
@@ -209,7 +212,7 @@ __global__ __launch_bounds__(B2G<LP>::THREADS, 4) void blk2_ab(BlkTables tb, Amp
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int c = blockIdx.x, cw = blockIdx.y, tid = threadIdx.x;
     if (!bf.active[cw]) return;
-    B2_SETPRIO(1);
+    B2_SETPRIO(B2_PRIO_REST);
     const float *beta = bf.beta + (size_t)cw * tb.LM + (size_t)c * tb.Mc;
     float bv[B2_J];
 #pragma unroll
@@ -228,7 +231,7 @@ __global__ __launch_bounds__(B2G<LP>::THREADS, 4) void blk2_az(BlkTables tb, Amp
     float *dr = reinterpret_cast<float *>(smem);
     const int c = blockIdx.x, cw = blockIdx.y, tid = threadIdx.x;
     if (!bf.active[cw]) return;
-    B2_SETPRIO(1);
+    B2_SETPRIO(B2_PRIO_REST);
     float u[B2_J];
 #pragma unroll
     for (int i = 0; i < B2_J; ++i) u[i] = 0.f;
@@ -270,9 +273,9 @@ __global__ __launch_bounds__(B2G<LP>::THREADS, 4) void blk2_az(BlkTables tb, Amp
             for (int g = tl + 2 * T; g < ng; g += T) row(tb.gk[g0 + g], gcw[g0 + g]);
             __syncthreads();
             // (stage twiddles from the hardware sine / cosine: no table entries in flight, u[] stays in registers)
-            B2_SETPRIO(0);
+            B2_SETPRIO(B2_PRIO_FFT);
             lds_fft1_sincos<true, 16, LP, 0, 4, true>(d, tl);
-            B2_SETPRIO(1);
+            B2_SETPRIO(B2_PRIO_REST);
             uint32_t pv[B2_J / 2];
             if (B2_ONETABLE) b2_pos_load1<LP>(tb, t, tl, pv);
             else b2_pos_load<LP>(tb, t, m2, tl, pv);

@@ -90,7 +90,8 @@ static_assert(C2_EPT == 16, "the transform is written for 16 values per thread")
 // slot, so a workgroup's chain waited behind the other's transform; with the chains at 1 over the
 // transforms at 0 the transform fills the chains' gaps instead: cw2_az 0.531 -> 0.501, cw2_ab 0.382 ->
 // 0.378 ms per launch, C2 probe 11.77 k -> 12.29 k codewords/s same box, identical results (priority 2 or
-// 3 for the chains, 2 for the statistics alone, or Az alone measured the same or less:
+// 3 for the chains, 2 for the statistics alone, or Az alone measured the same or less, and the gain is the
+// class-start phase's: with it at 0 and the rest at 1 the iteration is slower than flat;
 // profiles/r05_prio_ab.txt).  Both 0: flat, for the A/B.
 #ifndef C2_PRIO_FFT
 #define C2_PRIO_FFT 0
