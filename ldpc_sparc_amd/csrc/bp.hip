@@ -37,6 +37,13 @@ namespace sg {
 #endif
 constexpr int BP_PS_PAD = 2;
 
+// Single-precision min-sum: the check pass at issue priority 1 over the variable pass at 0 (the grouped
+// kernel's scheme; three workgroups share a CU): 1.456 -> 1.392 ms per launch on the C3 code (table kernel
+// forced), bit-identical.  Double-precision sumprod2 measured 1 % slower with it, so the other kinds stay
+// flat (profiles/r05_prio_ab.txt).  0: flat for every kind (A/B).
+#ifndef BPF_PRIO
+#define BPF_PRIO 1
+#endif
 template <typename T>
 __device__ __forceinline__ T dev_log(T x);
 template <>
@@ -320,6 +327,7 @@ __global__ __launch_bounds__(BP_THREADS, (bp_waves_per_simd<T, KIND>())) void bp
                 }
                 apv[j] = acc;
             }
+            if (BPF_PRIO && sizeof(T) == 4 && KIND == SG_MINSUM) __builtin_amdgcn_s_setprio(1);
             __syncthreads();
             // ---- check pass (c_ldpc.c:183-194)
             int unsat = 0;
@@ -342,6 +350,7 @@ __global__ __launch_bounds__(BP_THREADS, (bp_waves_per_simd<T, KIND>())) void bp
                     if (d1 > 0) unsat |= check_update_from<T, KIND, MAXDC>(msg, c1, a.nc, d1, a.factor, L1) ? 1 : 0;
                 }
             }
+            if (BPF_PRIO && sizeof(T) == 4 && KIND == SG_MINSUM) __builtin_amdgcn_s_setprio(0);
             if (!__syncthreads_or(unsat)) break;  // c_ldpc.c:196-197
         }
         T *out = a.app + (size_t)cw * a.nv;
