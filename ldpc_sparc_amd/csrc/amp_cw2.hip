@@ -131,6 +131,12 @@ __device__ __forceinline__ int c2_opaque(int v) {
     return v;
 }
 
+// the first transform stage's stale-value masks as v_bfe_i32 + v_and (1), or as the compiler's own
+// compare + select (0) (A/B)
+#ifndef C2_MASK_BFE
+#define C2_MASK_BFE 1
+#endif
+
 // w_N2^j = exp(-2 pi i j / N2) from the hardware sine / cosine (revolutions;
 // (j mod N2) / N2 is exact in f32 for N2 <= 2^19)
 __device__ __forceinline__ cx<float> c2_w(const Cw2Tables &tb, uint32_t j) {
@@ -260,10 +266,15 @@ __device__ __forceinline__ void c2_stage0_r32(int tid, uint32_t msk) {
 #pragma unroll
     for (int jj = 0; jj < 16; ++jj) v[jj] = src[264 * jj];
 #pragma unroll
-    for (int jj = 0; jj < 16; ++jj) {  // all-ones / zero from the sign-extended bit
-        const uint32_t mx = (uint32_t)((int)(msk << (31 - 2 * jj)) >> 31);
-        const uint32_t my = (uint32_t)((int)(msk << (30 - 2 * jj)) >> 31);
-        v[jj] = c2f{__uint_as_float(__float_as_uint(v[jj].x) & mx), __uint_as_float(__float_as_uint(v[jj].y) & my)};
+    for (int jj = 0; jj < 16; ++jj) {  // all-ones / zero from the sign-extended bit (v_bfe_i32)
+        int mx = __builtin_amdgcn_sbfe((int)msk, 2 * jj, 1), my = __builtin_amdgcn_sbfe((int)msk, 2 * jj + 1, 1);
+#if C2_MASK_BFE
+        // (opaque: otherwise the compiler turns bit-extract-and-AND back into a compare and a select per
+        // component, serialised on VCC with hazard nops -- 3 VALU and a nop instead of 2 VALU)
+        asm volatile("" : "+v"(mx), "+v"(my));
+#endif
+        v[jj] = c2f{__uint_as_float(__float_as_uint(v[jj].x) & (uint32_t)mx),
+                    __uint_as_float(__float_as_uint(v[jj].y) & (uint32_t)my)};
     }
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) c2_swap32(v[jj], v[jj + 8]);  // lane half H: x[J], x[16 + J], J = jj + 8 H
@@ -977,8 +988,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
 #pragma unroll
             for (int i = 0; i < RC; ++i) x[i] = sgp[i];
 #pragma unroll
-            for (int i = 0; i < RC; ++i) {  // -inf past the segment by a sign mask and v_bfi (a compare and a
-                                            // select would serialise on one SGPR pair with hazard nops)
+            for (int i = 0; i < RC; ++i) {  // -inf past the segment by a sign mask and v_bfi
                 const uint32_t mk = (uint32_t)((i - n) >> 31);  // all ones inside the segment
                 x[i] = __uint_as_float((__float_as_uint(x[i]) & mk) | (0xff800000u & ~mk));
             }

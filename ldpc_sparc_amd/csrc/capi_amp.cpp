@@ -489,6 +489,73 @@ static int build_cw(sg_amp_plan *p, const std::vector<int32_t> &row_k1, const st
     return SG_OK;
 }
 
+// Bank-aware placement of the conjugate row pairs on the split engine's threads (amp_cw2.hip: at slot j
+// the lanes of each 32-lane half of a wavefront read rows r and P - r of their slot's pair with
+// ds_read_b64, bank pair c2pos(row) mod 32, in cw2_ab's accumulation, and write them in cw2_az's rows).
+// Local search from the load-balanced placement, as cw_bank_balance: swap two pairs of the same length
+// that start at the same slot of threads in different lane groups when the summed worst bank multiplicity
+// of the cells they touch does not grow.  Every output keeps its arithmetic (same slot structure per
+// thread, same class order); only the order of cw2_ctrl's sum of z^2 (phi) follows the placement.
+// Deterministic (fixed seed).
+#ifndef CW2_BANKBAL
+#define CW2_BANKBAL 1
+#endif
+static void cw2_bank_balance(std::vector<std::vector<int>> &own, const std::vector<std::vector<int>> &pair_of,
+                             int OT, int P) {
+    const int T = CW2_THREADS;
+    std::vector<int> at((size_t)T * OT, -1), pos((size_t)T * OT, -1), start((size_t)T * OT, 0);
+    for (int t = 0; t < T; ++t) {
+        int j = 0;
+        for (int i = 0; i < (int)own[t].size(); ++i) {
+            const int r = own[t][i], len = (int)pair_of[r].size();
+            start[(size_t)t * OT + j] = len;
+            for (int q = 0; q < len; ++q, ++j) {
+                at[(size_t)t * OT + j] = r;
+                pos[(size_t)t * OT + j] = i;
+            }
+        }
+    }
+    // the lanes of a group hold distinct pairs at a slot, so distinct rows; empty slots all read row 0
+    auto cell = [&](int g, int j) {
+        int ca[32] = {0}, cb[32] = {0}, wa = 0, wb = 0;
+        bool empty = false;
+        for (int l = 0; l < 32; ++l) {
+            const int r = at[(size_t)(g * 32 + l) * OT + j];
+            if (r < 0) {
+                if (empty) continue;
+                empty = true;
+            }
+            const int ra = r < 0 ? 0 : r, rb = r < 0 ? 0 : (P - r) % P;
+            wa = std::max(wa, ++ca[c2pos(ra) & 31]);
+            if (rb != ra) wb = std::max(wb, ++cb[c2pos(rb) & 31]);
+        }
+        return wa + wb;
+    };
+    std::vector<std::vector<int>> by((size_t)OT * (OT + 1));
+    for (int t = 0; t < T; ++t)
+        for (int j = 0; j < OT; ++j)
+            if (const int len = start[(size_t)t * OT + j]) by[(size_t)j * (OT + 1) + len].push_back(t);
+    std::mt19937 rng(12345);
+    const int iters = 8 * T * OT;
+    for (int it = 0; it < iters; ++it) {
+        const int A = (int)(rng() % T), j = (int)(rng() % OT), len = start[(size_t)A * OT + j];
+        if (!len) continue;
+        const auto &cand = by[(size_t)j * (OT + 1) + len];
+        const int B = cand[rng() % cand.size()];
+        const int gA = A / 32, gB = B / 32;
+        if (gA == gB) continue;
+        int before = 0, after = 0;
+        for (int q = j; q < j + len; ++q) before += cell(gA, q) + cell(gB, q);
+        for (int q = j; q < j + len; ++q) std::swap(at[(size_t)A * OT + q], at[(size_t)B * OT + q]);
+        for (int q = j; q < j + len; ++q) after += cell(gA, q) + cell(gB, q);
+        if (after > before) {
+            for (int q = j; q < j + len; ++q) std::swap(at[(size_t)A * OT + q], at[(size_t)B * OT + q]);
+            continue;
+        }
+        std::swap(own[A][pos[(size_t)A * OT + j]], own[B][pos[(size_t)B * OT + j]]);
+    }
+}
+
 // Split per-codeword engine tables (amp_cw2.hip).  Output i at DCT position
 // K reads H[a] and H[b], b = N2 - a (fwd_coef), and its inverse input adds to
 // G[a] and G[b] (inv_contrib: first call a, second b): both touch only the
@@ -558,6 +625,7 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
     }
     if (OT > 16) return SG_OK;  // kernel instances for 12, 13, 14 and 16 outputs per thread
     OT = OT <= 12 ? 12 : OT <= 14 ? OT : 16;
+    if (CW2_BANKBAL) cw2_bank_balance(own, pair_of, OT, P);
     std::vector<uint32_t> ka((size_t)OT * T, 0u);
     std::vector<int32_t> oi((size_t)OT * T, 0);
     std::vector<float> cf((size_t)OT * T * 4, 0.f), gf((size_t)OT * T * 4, 0.f);

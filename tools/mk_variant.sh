@@ -7,7 +7,7 @@ cd "$(dirname "$0")/.."
 name=$1; src=$2; shift 2
 C=ldpc_sparc_amd/csrc; O=ldpc_sparc_amd/_lib/obj; D=ldpc_sparc_amd/_lib_v_$name
 mkdir -p $D/obj
-base=$(basename $src .hip)
+base=$(basename $(basename $src .hip) .cpp)
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Wno-unused-value --offload-arch=gfx950 \
   -Iinclude "$@" -x hip -c $C/$src -o $D/obj/$base.o
 objs=$(ls $O/*.o | grep -v "/$base.o$")
