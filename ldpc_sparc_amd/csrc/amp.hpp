@@ -249,6 +249,8 @@ struct Cw2Tables {
 };
 int cw2_launch_iter(const Cw2Tables &tb, const RegBufs<float> &bf, const AmpScalars &sc, const AmpParams &pr, int t,
                     hipStream_t s);
+// z in natural order from the split engine's slot-order copy (before a hand-over to the staged engine)
+int cw2_launch_z_natural(const Cw2Tables &tb, const RegBufs<float> &bf, hipStream_t s);
 // The same engine in double precision (amp_cw2d.hip): the split engine's slot and class tables, double
 // coefficients, the slots' w_N2^a (Horner / rotation steps over the classes) and the P-point stage twiddles.
 // One 512-thread workgroup per CU (the complex double image is 132 KB).

@@ -581,7 +581,6 @@ __global__ __launch_bounds__(C2_T) void cw2_ctrl(Cw2Tables tb, RegBufs<float> bf
     if (!bf.active[cw]) return;
     const bool have_beta = t > 0;
     double *psi = sc.psi + cw, *psi_prev = sc.psi_prev + cw;
-    float *z = bf.z + (size_t)cw * tb.n;
     const float *y = bf.y + (size_t)cw * tb.n;
     const bool sum_z = pr.phi_method != 1;
     double g;
@@ -609,13 +608,11 @@ __global__ __launch_bounds__(C2_T) void cw2_ctrl(Cw2Tables tb, RegBufs<float> bf
         // every load first, in one round trip (the uniform branch outside the slot loops: written per slot,
         // with the stores between, the compiler waited for each slot's loads in turn -- 36 dependent round
         // trips per launch); invalid slots: output 0, unused
-        int oi[OT];
         uint32_t kv[OT];
         float yv[OT], zv[OT], r0[OT], r1[OT];
         float *ys = tb.ys + (size_t)cw * OT * C2_T, *zs = tb.zs + (size_t)cw * OT * C2_T;
 #pragma unroll
         for (int j = 0; j < OT; ++j) {
-            oi[j] = tb.oi[j * C2_T + tid];
             kv[j] = tb.ka[j * C2_T + tid];
             if constexpr (C2_POLAR != 0) gmv[j] = tb.gm[j * C2_T + tid];
         }
@@ -632,20 +629,20 @@ __global__ __launch_bounds__(C2_T) void cw2_ctrl(Cw2Tables tb, RegBufs<float> bf
                 zr[j] = (yv[j] - (r0[j] + r1[j])) + bco * zv[j];
         } else {  // first iteration: gather y and keep it in slot order
 #pragma unroll
-            for (int j = 0; j < OT; ++j) yv[j] = y[oi[j]];
+            for (int j = 0; j < OT; ++j) yv[j] = y[tb.oi[j * C2_T + tid]];
 #pragma unroll
             for (int j = 0; j < OT; ++j) {
                 ys[j * C2_T + tid] = yv[j];
                 zr[j] = yv[j];
             }
         }
+        // z in slot order only: a hand-over to the staged engine rebuilds its natural order once
+        // (cw2_z_natural); scattered here every iteration it cost 12 index loads and 12 scattered stores
+        // per thread
 #pragma unroll
         for (int j = 0; j < OT; ++j) {
             zs[j * C2_T + tid] = zr[j];
-            if (kv[j] & CW_VALID) {
-                z[oi[j]] = zr[j];  // (natural order: the staged engine's after a hand-over)
-                if (sum_z) acc += (double)zr[j] * (double)zr[j];
-            }
+            if ((kv[j] & CW_VALID) && sum_z) acc += (double)zr[j] * (double)zr[j];
         }
     }
     double phi;
@@ -1180,6 +1177,23 @@ __global__ __launch_bounds__(1024) void cw2_merge(Cw2Tables tb, RegBufs<float> b
             bf.active[cw] = 0;
         }
     }
+}
+
+// z of every codeword in natural order from its slot-order copy (cw2_ctrl keeps z in slot order only): run
+// once, at a hand-over to the staged engine, whose control kernel reads z in natural order
+__global__ __launch_bounds__(C2_T) void cw2_z_natural(Cw2Tables tb, RegBufs<float> bf) {
+    const int cw = blockIdx.x, tid = threadIdx.x;
+    const float *zs = tb.zs + (size_t)cw * tb.OT * C2_T;
+    float *z = bf.z + (size_t)cw * tb.n;
+    for (int j = 0; j < tb.OT; ++j)
+        if (tb.ka[j * C2_T + tid] & CW_VALID) z[tb.oi[j * C2_T + tid]] = zs[j * C2_T + tid];
+}
+
+int cw2_launch_z_natural(const Cw2Tables &tb, const RegBufs<float> &bf, hipStream_t s) {
+    if (bf.B <= 0) return SG_OK;
+    hipLaunchKernelGGL(cw2_z_natural, dim3(bf.B), dim3(C2_T), 0, s, tb, bf);
+    SG_HIP(hipGetLastError());
+    return SG_OK;
 }
 
 template <int OT>

@@ -1612,6 +1612,8 @@ static int decode_regular(sg_amp_plan *p, const void *d_y, int B, const int32_t 
         if (na > 0 && cw && !cw_forced && na < handover * B) {
             cw = false;
             p->last_handover = t + 1;  // first iteration on the staged engine
+            if constexpr (std::is_same<T, float>::value)  // (the split engine keeps z in slot order only)
+                if (use_cw2(p)) SG_TRY(cw2_launch_z_natural(c2tables(p, B), bf, s));
         }
         if (t % 4 == 3 && t + 2 < t_max - 1 && !tb.skip) SG_TRY(poll.request());
     }
