@@ -573,6 +573,28 @@ __device__ __forceinline__ double c2_block_sum(double v, double *red) {
     return t;
 }
 
+// two sums at once (one pair of barriers), each in c2_block_sum's order
+__device__ __forceinline__ void c2_block_sum2(double &a, double &b, double *red) {
+    for (int o = 32; o > 0; o >>= 1) {
+        a += __shfl_xor(a, o, 64);
+        b += __shfl_xor(b, o, 64);
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (int)(blockDim.x >> 6);
+    __syncthreads();
+    if (lane == 0) {
+        red[wid] = a;
+        red[nw + wid] = b;
+    }
+    __syncthreads();
+    double ta = 0.0, tb = 0.0;
+    for (int w = 0; w < nw; ++w) {
+        ta += red[w];
+        tb += red[nw + w];
+    }
+    a = ta;
+    b = tb;
+}
+
 template <int OT>
 __global__ __launch_bounds__(C2_T) void cw2_ctrl(Cw2Tables tb, RegBufs<float> bf, AmpScalars sc, AmpParams pr,
                                                  int t) {
@@ -608,14 +630,11 @@ __global__ __launch_bounds__(C2_T) void cw2_ctrl(Cw2Tables tb, RegBufs<float> bf
         // every load first, in one round trip (the uniform branch outside the slot loops: written per slot,
         // with the stores between, the compiler waited for each slot's loads in turn -- 36 dependent round
         // trips per launch); invalid slots: output 0, unused
-        uint32_t kv[OT];
         float yv[OT], zv[OT], r0[OT], r1[OT];
         float *ys = tb.ys + (size_t)cw * OT * C2_T, *zs = tb.zs + (size_t)cw * OT * C2_T;
 #pragma unroll
-        for (int j = 0; j < OT; ++j) {
-            kv[j] = tb.ka[j * C2_T + tid];
+        for (int j = 0; j < OT; ++j)
             if constexpr (C2_POLAR != 0) gmv[j] = tb.gm[j * C2_T + tid];
-        }
         if (have_beta) {  // y, the previous z and the two halves' parts in slot order: coalesced
 #pragma unroll
             for (int j = 0; j < OT; ++j) {
@@ -627,9 +646,12 @@ __global__ __launch_bounds__(C2_T) void cw2_ctrl(Cw2Tables tb, RegBufs<float> bf
 #pragma unroll
             for (int j = 0; j < OT; ++j)  // Onsager residual, sparc.py:943-946; r = Re(c1 H[a] + c2 conj H[b])
                 zr[j] = (yv[j] - (r0[j] + r1[j])) + bco * zv[j];
-        } else {  // first iteration: gather y and keep it in slot order
+        } else {  // first iteration: gather y and keep it in slot order, 0 in the invalid slots -- so their
+                  // z stays 0 in every iteration (their forward part is 0: zero coefficients) and they add
+                  // exact zeros to the sum below, which then needs no validity test
 #pragma unroll
-            for (int j = 0; j < OT; ++j) yv[j] = y[tb.oi[j * C2_T + tid]];
+            for (int j = 0; j < OT; ++j)
+                yv[j] = (tb.ka[j * C2_T + tid] & CW_VALID) ? y[tb.oi[j * C2_T + tid]] : 0.f;
 #pragma unroll
             for (int j = 0; j < OT; ++j) {
                 ys[j * C2_T + tid] = yv[j];
@@ -642,7 +664,7 @@ __global__ __launch_bounds__(C2_T) void cw2_ctrl(Cw2Tables tb, RegBufs<float> bf
 #pragma unroll
         for (int j = 0; j < OT; ++j) {
             zs[j * C2_T + tid] = zr[j];
-            if ((kv[j] & CW_VALID) && sum_z) acc += (double)zr[j] * (double)zr[j];
+            if (sum_z) acc += (double)zr[j] * (double)zr[j];
         }
     }
     double phi;
@@ -1110,7 +1132,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
 // ---------------------------------------------------------------------------- merge
 __global__ __launch_bounds__(1024) void cw2_merge(Cw2Tables tb, RegBufs<float> bf, AmpScalars sc, AmpParams pr,
                                                   int t) {
-    __shared__ double red[16];
+    __shared__ double red[32];
     const int cw = blockIdx.x, tid = threadIdx.x;
     if (!bf.active[cw]) return;
     const size_t lb = (size_t)cw * tb.L;
@@ -1154,8 +1176,7 @@ __global__ __launch_bounds__(1024) void cw2_merge(Cw2Tables tb, RegBufs<float> b
             }
         }
     }
-    a = c2_block_sum(a, red);
-    er = c2_block_sum(er, red);
+    c2_block_sum2(a, er, red);
     if (tid == 0) {
         double *psi = sc.psi + cw, *psi_prev = sc.psi_prev + cw;
         double *nmse = sc.nmse + (size_t)cw * pr.t_max;
