@@ -248,6 +248,32 @@ def test_c4_block_engine_vs_oracle():
     np.testing.assert_allclose(nm[0, :10], np.asarray(rn).reshape(40, -1)[:10], atol=2e-3)
 
 
+def test_c4_block_engine_batch_vs_oracle():
+    """A 32-codeword C4 batch through the shipped block engine (the bench's sc
+    line runs it at B = 256) against the CPU restatement on every codeword, the
+    restatement fanned out over the host cores (oracle/cpu_pool.py): the same
+    MAP decision on every section but at most 0.01 %, stopping iterations within
+    one (f32 against float64 with a float128 softmax), the same decoded
+    codewords."""
+    from oracle import cpu_pool
+    W, L, M, n, o0, o1 = _c4_design(5)
+    op = sparc.DesignOperator(W, L, M, n, o0, o1)
+    B = 32
+    rng = np.random.default_rng(17)
+    true = rng.integers(0, M, (B, L)).astype(np.int32)
+    beta0 = np.zeros((B, L * M))
+    beta0[np.arange(B)[:, None], np.arange(L) * M + true] = 1
+    Y = op.apply(beta0, False) + rng.standard_normal((B, n))
+    mi, tf, nm, _ = sparc.amp_decode_batch(Y, op, 1.0, 40, true_idx=true, precision=_native.SG_F32)
+    res, _ = cpu_pool.amp_decode(cpu_pool.host_cores(), W, L, M, n, o0, o1, Y, true, 40)
+    assert sorted(res) == list(range(B))
+    cpu_map = np.stack([res[b][0] for b in range(B)])
+    cpu_tf = np.array([res[b][1] for b in range(B)])
+    assert np.mean(mi != cpu_map) <= 1e-4
+    assert np.max(np.abs(tf.astype(int) - cpu_tf)) <= 1, (tf, cpu_tf)
+    assert np.array_equal((mi == true).all(1), (cpu_map == true).all(1))
+
+
 def test_c4_block_engine_vs_general_engine(monkeypatch):
     """The block engine and the general four-step engine (SG_AMP_ENGINE=general)
     decode the same C4 batch to the same decisions and stopping iterations."""
