@@ -55,22 +55,6 @@ static_assert(C2_EPT == 16, "the transform is written for 16 values per thread")
 #endif
 #define C2_SKIP(bit) ((C2_ABL & (bit)) != 0)
 
-// Start stagger (A/B: -DC2_STAGGER=<cycles> -DC2_STAGGER_SEL=<rule>): two workgroups share a CU and run
-// the same class loop; started together they stay in phase (both load, then both transform).  The
-// selected workgroups of the first wave sleep `cycles` at entry, about half a class, so one
-// workgroup's memory phases fall under the other's transform.  Rules: 0 the second half of the first
-// wave (blocks 256..511: the second slot of every CU if the dispatcher fills one per CU first), 1 the
-// odd blocks of the first wave, 2 every other block of an XCD (b & 8: blocks b and b + 8 share one).
-#ifndef C2_STAGGER
-#define C2_STAGGER 0
-#endif
-// Az statistics: the segment's reads unconditional (A/B); no argmax, the maximum's term dropped by fract (A/B)
-#ifndef C2_STATS_LOADS
-#define C2_STATS_LOADS 1
-#endif
-#ifndef C2_STATS_V2
-#define C2_STATS_V2 1
-#endif
 // Az rows: the row addresses from the slot's flags instead of the host table wab (A/B)
 #ifndef C2_ROWS_DERIVE
 #define C2_ROWS_DERIVE 1
@@ -107,19 +91,6 @@ static_assert(C2_EPT == 16, "the transform is written for 16 values per thread")
 #ifndef C2_AB_PF
 #define C2_AB_PF 1
 #endif
-#ifndef C2_STAGGER_SEL
-#define C2_STAGGER_SEL 0
-#endif
-__device__ __forceinline__ void c2_stagger() {
-    if (C2_STAGGER <= 0) return;
-    const int b = blockIdx.x;
-    bool late;
-    if (C2_STAGGER_SEL == 0) late = b >= 256 && b < 512;
-    else if (C2_STAGGER_SEL == 1) late = b < 512 && (b & 1);
-    else late = b < 512 && (b & 8);
-    if (late)
-        for (int c = 0; c < C2_STAGGER; c += 8128) __builtin_amdgcn_s_sleep(127);
-}
 
 // exp(x / tau) as exp2(x * (log2 e / tau)): __expf lowers to a multiply by log2 e and v_exp_f32, so
 // with log2 e folded into the per-codeword scale every exponential is one instruction
@@ -434,7 +405,6 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
     c2f *sMI = reinterpret_cast<c2f *>(smem + C2_IMG_BYTES);  // previous beta's (section max, 1 / sum)
     const int h = blockIdx.x & 1, cw = blockIdx.x >> 1, tid = threadIdx.x;
     if (!bf.active[cw]) return;
-    c2_stagger();
     C2_SETPRIO(C2_PRIO_REST);
     const size_t lb = (size_t)cw * tb.L;
     for (int l = tid; l < tb.L; l += C2_T) {  // previous beta's section max, 1/sum
@@ -730,7 +700,6 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
     float *dr = reinterpret_cast<float *>(smem);
     const int h = blockIdx.x & 1, cw = blockIdx.x >> 1, tid = threadIdx.x;
     if (!bf.active[cw]) return;
-    c2_stagger();
     C2_SETPRIO(C2_PRIO_REST);
     const size_t lb = (size_t)cw * tb.L;
     const bool have_beta = t > 0;
@@ -1000,7 +969,6 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
             constexpr int RC = 16;
             const float *sgp = dr + a;  // inside the LDS image past the segment's end too
             float x[RC];
-#if C2_STATS_LOADS
             // every read unconditional, the entries past the segment masked afterwards: written as
             // `i < n ? sgp[i] : -inf` the compiler put each read in its own exec-masked block (two SALU
             // mask operations per read, no paired reads)
@@ -1011,11 +979,6 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
                 const uint32_t mk = (uint32_t)((i - n) >> 31);  // all ones inside the segment
                 x[i] = __uint_as_float((__float_as_uint(x[i]) & mk) | (0xff800000u & ~mk));
             }
-#else
-#pragma unroll
-            for (int i = 0; i < RC; ++i) x[i] = i < n ? sgp[i] : -INFINITY;
-#endif
-#if C2_STATS_V2
             // no argmax: the maximum by a max3 tree; in the sums, v_fract_f32 drops the entries equal to the
             // maximum (e = exp2(0) = 1 exactly, fract 0; below it e < 1, fract(e) = e) and the entries that
             // tie with it are added back afterwards from Se - S1 = their count (exact small integers), so
@@ -1060,47 +1023,6 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
                     S2 += ties;
                 }
             }
-#else
-            float m = -INFINITY;
-            int am = -1;
-#pragma unroll
-            for (int i = 0; i < RC; ++i) {
-                const bool up = x[i] > m;
-                m = up ? x[i] : m;
-                am = up ? i : am;
-            }
-            for (int c = RC; c < n; c += RC) {
-                float y[RC];
-#pragma unroll
-                for (int i = 0; i < RC; ++i) y[i] = dr[a + c + i];
-#pragma unroll
-                for (int i = 0; i < RC; ++i) {
-                    const bool up = c + i < n && y[i] > m;
-                    m = up ? y[i] : m;
-                    am = up ? c + i : am;
-                }
-            }
-            float S1 = 0.f, S2 = 0.f;
-#pragma unroll
-            for (int i = 0; i < RC; ++i) {
-                float ex = c2_exp2((x[i] - m) * inv_tau);
-                ex = i != am ? ex : 0.f;
-                S1 += ex;
-                S2 += ex * ex;
-            }
-            for (int c = RC; c < n; c += RC) {
-                float y[RC];
-#pragma unroll
-                for (int i = 0; i < RC; ++i) y[i] = dr[a + c + i];
-#pragma unroll
-                for (int i = 0; i < RC; ++i) {
-                    float ex = c2_exp2((y[i] - m) * inv_tau);
-                    ex = (c + i < n && c + i != am) ? ex : 0.f;
-                    S1 += ex;
-                    S2 += ex * ex;
-                }
-            }
-#endif
             if (m > -INFINITY) {  // merge into the section's running statistics
                 if (m > Mr[k]) {
                     const float f = c2_exp2((Mr[k] - m) * inv_tau);
