@@ -650,6 +650,11 @@ __global__ __launch_bounds__(D_T, 1) void cw2d_az(Cw2dTables tb, RegBufs<double>
 // One wavefront per section (a segment of it per class: a contiguous run of s in class order, about
 // LM / (Q L) = 8 entries; Q <= 64, M <= 512): every entry read once from HBM, one exponential per
 // entry, sums in a fixed order (per lane, then a xor-shuffle tree).
+// the class of each entry from a per-section owner table each class's lane fills (1), or a binary search
+// over the classes' prefix sums per entry (0) (A/B)
+#ifndef D_ST_OWNER
+#define D_ST_OWNER 1
+#endif
 constexpr int ST_WAVES = 4;  // sections per 256-thread workgroup
 constexpr int ST_K = 8;      // entries per lane: sections of M <= 512 entries
 __device__ __forceinline__ double d_wave_max(double v) {
@@ -667,6 +672,9 @@ __global__ __launch_bounds__(64 * ST_WAVES) void cw2d_stats(Cw2dTables tb, RegBu
     // (class-order position minus that prefix): entry k of the section lives at base[m] + k, m the last
     // class with prefix[m] <= k
     __shared__ int pre[ST_WAVES][64], bas[ST_WAVES][64];
+#if D_ST_OWNER
+    __shared__ uint8_t own[ST_WAVES][64 * ST_K];  // the class of each entry of the section
+#endif
     const int wpc = tb.L / ST_WAVES;  // workgroups per codeword
     const int w = (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int cw = blockIdx.x / wpc, l = (blockIdx.x % wpc) * ST_WAVES + w;
@@ -690,20 +698,29 @@ __global__ __launch_bounds__(64 * ST_WAVES) void cw2d_stats(Cw2dTables tb, RegBu
     const int total = __shfl(inc, 63, 64);  // the section's entries (M)
     pre[w][lane] = inc - n;
     bas[w][lane] = p0 - (inc - n);
+#if D_ST_OWNER
+    for (int k = inc - n; k < inc; ++k) own[w][k] = (uint8_t)lane;  // each class marks its segment's entries
+#endif
     __syncthreads();
     // the section's entries k = lane + 64 j in concatenated class order: consecutive lanes read consecutive
     // positions of a segment (coalesced runs), no padding, one exponential per entry
+#if !D_ST_OWNER
     const int nq = tb.Q;
+#endif
     int ad[ST_K];
     double x[ST_K];
 #pragma unroll
     for (int j = 0; j < ST_K; ++j) {
         const int k = lane + 64 * j;
+        const bool in = k < total;
+#if D_ST_OWNER
+        const int lo = in ? (int)own[w][k] : 0;  // (one LDS read instead of a six-step search)
+#else
         int lo = 0;
 #pragma unroll
         for (int step = 32; step > 0; step >>= 1)  // last class with pre <= k (empty classes: same pre)
             if (lo + step < nq && pre[w][lo + step] <= k) lo += step;
-        const bool in = k < total;
+#endif
         ad[j] = in ? bas[w][lo] + k : 0;
         x[j] = d_keep(s[ad[j]], k, total, 0xfff00000u);  // past the section: -inf
     }
