@@ -655,7 +655,14 @@ __global__ __launch_bounds__(D_T, 1) void cw2d_az(Cw2dTables tb, RegBufs<double>
 #ifndef D_ST_OWNER
 #define D_ST_OWNER 1
 #endif
-constexpr int ST_WAVES = 4;  // sections per 256-thread workgroup
+// sections per workgroup (one wavefront each): the widest of 16, 8, 4 that divides L, at most D_ST_MAXW.  A
+// workgroup's sections are consecutive, so its wavefronts read and write neighbouring segments of every
+// class -- neighbouring cache lines -- together.  Same box, f64 iteration (ms): 4 sections 2.392, 8 2.310,
+// 16 2.198 (2: 2.493), decisions bit-identical (profiles/r05_f64_ablation.txt)
+#ifndef D_ST_MAXW
+#define D_ST_MAXW 16
+#endif
+constexpr int ST_WAVES_MIN = 4;
 constexpr int ST_K = 8;      // entries per lane: sections of M <= 512 entries
 __device__ __forceinline__ double d_wave_max(double v) {
 #pragma unroll
@@ -667,6 +674,7 @@ __device__ __forceinline__ double d_wave_sum(double v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+template <int ST_WAVES>
 __global__ __launch_bounds__(64 * ST_WAVES) void cw2d_stats(Cw2dTables tb, RegBufs<double> bf) {
     // per wavefront: exclusive prefix of the segment lengths over the classes, and each segment's base
     // (class-order position minus that prefix): entry k of the section lives at base[m] + k, m the last
@@ -823,7 +831,12 @@ static int cw2d_launch(const Cw2dTables &tb, const RegBufs<double> &bf, const Am
     }
     {
         ProfScope ps(SG_PH_CW2_CTRL, s);
-        hipLaunchKernelGGL((cw2d_stats), dim3(bf.B * (tb.L / ST_WAVES)), dim3(64 * ST_WAVES), 0, s, tb, bf);
+        if (D_ST_MAXW >= 16 && tb.L % 16 == 0)
+            hipLaunchKernelGGL((cw2d_stats<16>), dim3(bf.B * (tb.L / 16)), dim3(64 * 16), 0, s, tb, bf);
+        else if (D_ST_MAXW >= 8 && tb.L % 8 == 0)
+            hipLaunchKernelGGL((cw2d_stats<8>), dim3(bf.B * (tb.L / 8)), dim3(64 * 8), 0, s, tb, bf);
+        else
+            hipLaunchKernelGGL((cw2d_stats<4>), dim3(bf.B * (tb.L / 4)), dim3(64 * 4), 0, s, tb, bf);
         hipLaunchKernelGGL((cw2d_final), gB, dim3(1024), 0, s, tb, bf, sc, pr, t);
     }
     return SG_OK;
@@ -832,7 +845,7 @@ static int cw2d_launch(const Cw2dTables &tb, const RegBufs<double> &bf, const Am
 int cw2d_launch_iter(const Cw2dTables &tb, const RegBufs<double> &bf, const AmpScalars &sc, const AmpParams &pr,
                      int t, hipStream_t s) {
     if (bf.B <= 0) return SG_OK;
-    if (tb.Q % 2 || tb.Q > 64 || tb.L > 1024 || tb.L % ST_WAVES || tb.Lblk != tb.L || tb.maxcls > CW2_SLICE ||
+    if (tb.Q % 2 || tb.Q > 64 || tb.L > 1024 || tb.L % ST_WAVES_MIN || tb.Lblk != tb.L || tb.maxcls > CW2_SLICE ||
         tb.M > 64 * ST_K ||
         tb.N2 != D_P * tb.Q || tb.M <= 0)
         return fail(SG_ERR_UNSUPPORTED, "f64 split engine: sizes outside its compile-time bounds");
