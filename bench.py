@@ -133,6 +133,8 @@ def parse():
                     help="launch/rendezvous only (no GPU): rank 0 prints the ranks that joined")
     ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
     ap.add_argument("--seed", type=int, default=1, help="Philox key of the synthetic inputs (stream = rank)")
+    ap.add_argument("--detail-dir", default="profiles",
+                    help="directory of bench_detail_<libsha>.json, the full per-configuration record")
     return ap.parse_args()
 
 
@@ -396,6 +398,7 @@ def amp_decodable(args, d, comm, cpu_seconds, procs):
     a = argparse.Namespace(**{**vars(args), "rate": rate})
     amp_step(st, a, comm)
     _native.device_synchronize()
+    prof = _native.Profiler(level=2)  # events around every AMP iteration, as the headline
     d.barrier()
     t0 = time.perf_counter()
     steps = max(1, args.steps // 2)
@@ -403,13 +406,23 @@ def amp_decodable(args, d, comm, cpu_seconds, procs):
         amp_step(st, a, comm)
     _native.device_synchronize()
     el = d.max(time.perf_counter() - t0)
+    phases = prof.stop()
     cnt = st["d_cnt"].download(np.zeros(4, np.int64))
     tf = st["d_tf"].download(np.zeros(st["B"], np.int32))
+    amp_ms = sum(phases.get(p, (0.0, 0))[0] for p in AMP_PHASES)
+    w = int(st["op"].w)
+    flops_per_cwit = 2 * 2.5 * w * np.log2(w) + 20 * st["L"] * st["M"]
+    tfl = flops_per_cwit * int(tf.sum()) * steps / (amp_ms * 1e-3) / 1e12 if amp_ms > 0 else None
     out = {"workload": f"C2 at R={rate}: L=1024, M=512, n={st['n']}, same design family, t_max={args.t_max}",
            "value": d.world * st["B"] * steps / el, "unit": "codewords/s", "batch_per_gpu": st["B"],
            "avg_iterations": float(tf.mean()), "section_errors": int(cnt[0]), "bit_errors": int(cnt[1]),
            "codeword_errors": int(cnt[2]),
-           "ber": float(cnt[1]) / (d.world * st["B"] * st["L"] * st["logM"])}
+           "ber": float(cnt[1]) / (d.world * st["B"] * st["L"] * st["logM"]),
+           "roofline": {"bound": "valu-f32", "achieved": tfl, "peak": VALU_PEAK_TFS, "unit": "TFLOP/s",
+                        "frac": tfl / VALU_PEAK_TFS if tfl else None,
+                        "algorithmic_flops_per_codeword_iteration": flops_per_cwit,
+                        "kernel_ms": {k: round(v[0], 3) for k, v in phases.items()},
+                        "launches": {k: v[1] for k, v in phases.items()}}}
     if cpu_seconds > 0:
         out["cpu_baseline"] = amp_cpu_baseline(st, a, cpu_seconds, procs)
     return out
@@ -609,9 +622,15 @@ def bp_variant(args, d, std, rate, z, dectype, prec, ebn0, B, steps, max_it=50, 
     fe = int((hard[:, :c.K] != X[:, :c.K]).any(1).sum())
     out = {"workload": f"{std} r{rate} z={z} (n={c.N}, max check degree {int(c.cdeg.max())}), {dectype}, "
                        f"{'f32' if prec == _native.SG_F32 else 'f64'}, max {max_it} it, Eb/N0 {ebn0} dB, random codewords",
-           "value": d.world * B * steps / el, "unit": "codewords/s", "batch_per_gpu": B,
+           "value": d.world * B * steps / el, "unit": "codewords/s", "batch_per_gpu": B, "ebn0": ebn0,
            "avg_executed_iterations": float(np.where(its < max_it, its + 1, max_it).mean()),
            "frame_errors": fe, "kernel_ms_per_launch": ph.get("bp_flood", (0.0, 1))[0] / max(ph.get("bp_flood", (0, 1))[1], 1)}
+    if prec == _native.SG_F32 and out["kernel_ms_per_launch"] > 0:  # LDS bound, as the C3 line
+        cwit = float(np.where(its < max_it, its + 1, max_it).sum())
+        lach = 16 * c.Nmsg * cwit / (out["kernel_ms_per_launch"] * 1e-3) / 1e9
+        lpk = bp_lds_peak_gbs(_native.cu_count())
+        out["roofline"] = {"bound": "lds", "achieved": lach, "peak": lpk, "unit": "GB/s", "frac": lach / lpk,
+                           "kernel": c.decode_kernel(dectype, prec)}
     if cpu_seconds > 0:
         from oracle import cpu_pool
         capp, cit, done, cel = cpu_pool.bp_decode(procs, dectype, ch, c.vdeg, c.cdeg, c.intrlv, max_it, 0.7,
@@ -787,7 +806,7 @@ def concat_bench(args, d):
     return {"workload": f"C5: SPARC(L=1024, M=512, n={n}, dense Gaussian design shared by the batch) + "
                         "4 x LDPC 802.11n r1/2 z=81 semi-protected (160 uncoded sections); AMP 25 it, "
                         "glue, sumprod2 BP 200 it; batch generated on the GPU (Philox, device LDPC encoder)",
-            "value": d.world * B * args.concat_steps / el, "unit": "codewords/s", "batch_per_gpu": B,
+            "value": d.world * B * args.concat_steps / el, "unit": "codewords/s", "batch_per_gpu": B, "n": n,
             "ebn0_db": args.concat_ebn0, "awgn_var": var, "R_overall": R_overall,
             "ber": float(cnt[1]) / (cnt[0] * user_bits) if cnt[0] else None,
             "codeword_errors": int(cnt[2]), "codewords": int(cnt[0]),
@@ -895,6 +914,123 @@ def summary(out):
     rf = out.get("roofline") or {}
     s["C2_factors"] = {"valu_issue": r(rf.get("valu_issue_frac")), "flops_per_lane": r(rf.get("flops_per_lane_instr"))}
     return {k: v for k, v in s.items() if v is not None}
+
+
+LINE_MAX_BYTES = 8192  # the driver ingests one stdout line; round 5's 23 KB line did not parse
+
+
+def _r(x, n=4):
+    return None if x is None else float(f"{x:.{n}g}")
+
+
+def _companion(o, frac=None, traffic_ratio=None, cpu_match=None):
+    """<= 150 B: value, roofline fraction, measured/algorithmic traffic, CPU decision match."""
+    if not isinstance(o, dict):
+        return None
+    rf = o.get("roofline") or {}
+    e = {"value": _r(o.get("value"), 5), "frac": _r(frac if frac is not None else rf.get("frac"), 3)}
+    if traffic_ratio is not None:
+        e["traffic_ratio"] = _r(traffic_ratio, 3)
+    if cpu_match is not None:
+        e["cpu_match"] = _r(cpu_match, 6)
+    return e
+
+
+def _bm(o, key):
+    cb = (o or {}).get("cpu_baseline") or {}
+    return (cb.get("ber_match") or cb).get(key)
+
+
+def compact_line(out, detail_rel):
+    """The one JSON line rank 0 prints (< LINE_MAX_BYTES): the contract keys, the
+    C2 roofline and cpu_baseline, and one short entry per companion
+    configuration; everything else goes to the detail file named in the line."""
+    keys = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype")
+    line = {k: out.get(k) for k in keys}
+    cfg = out.get("config") or {}
+    line["data"] = "synthetic: Philox messages, x = A beta0, AWGN sigma^2=1, generated on the GPU, resident in HBM"
+    line["config"] = {k: cfg.get(k) for k in ("workload", "L", "M", "n", "R", "t_max", "batch_per_gpu",
+                                               "parallelism", "counter_allreduce", "engine")}
+    rf = out.get("roofline") or {}
+    hb = out.get("roofline_hbm") or {}
+    tr = rf.get("traffic_per_codeword_iteration")
+    line["roofline"] = {
+        "bound": rf.get("bound"), "achieved": _r(rf.get("achieved"), 5), "peak": rf.get("peak"),
+        "unit": rf.get("unit"), "frac": _r(rf.get("frac"), 4), "traffic": _r(rf.get("traffic"), 5),
+        "traffic_unit": "HBM bytes per launch (PMC of this build; 1 launch = 1 AMP iteration of the batch)",
+        "traffic_over_algorithmic": _r(tr / hb["algorithmic_bytes_per_codeword_iteration"], 3)
+        if (tr and hb.get("algorithmic_bytes_per_codeword_iteration")) else None,
+        "valu_issue_frac": _r(rf.get("valu_issue_frac"), 3),
+        "flops_per_lane_instr": _r(rf.get("flops_per_lane_instr"), 3),
+        "lds_bank_conflict_frac": _r(rf.get("lds_bank_conflict_frac"), 3),
+        "kernel": "cw2_ab+cw2_ctrl+cw2_az+cw2_merge (amp_cw2.hip)" if "split" in str(rf.get("engine")) else
+        rf.get("kernel"),
+        "algorithmic_flops_per_codeword_iteration": rf.get("algorithmic_flops_per_codeword_iteration"),
+        "codeword_iterations_per_launch": _r(rf.get("codeword_iterations_per_launch"), 4),
+        "hbm_frac": _r(hb.get("frac"), 3), "lib_sha256": rf.get("lib_sha256")}
+    cb = out.get("cpu_baseline")
+    if cb:
+        bm = cb.get("ber_match") or {}
+        line["cpu_baseline"] = {
+            "value": _r(cb.get("value"), 4), "unit": cb.get("unit"), "cores": cb.get("cores"),
+            "kind": cb.get("kind"),
+            "sample": "%s of the %s C2 codewords the GPU decoded, oracle/sparc_ref.py (float128 softmax), "
+                      "1 thread per core" % (bm.get("codewords"), cfg.get("batch_per_gpu")),
+            "port_over_reference_speed": _r((cb.get("vs_reference") or {}).get("port_over_reference_speed"), 3),
+            "ber_match": {k: _r(bm.get(k), 7) if isinstance(bm.get(k), float) else bm.get(k)
+                          for k in ("codewords", "cpu_ber", "gpu_ber", "cpu_fer", "gpu_fer",
+                                    "identical_section_decisions", "t_final_equal",
+                                    "outside_2_at_reference_threshold", "outside_2_unexplained")}}
+    else:
+        line["cpu_baseline"] = None
+    comp = {}
+
+    def tratio(o):
+        rr = (o or {}).get("roofline") or {}
+        t, a = rr.get("traffic"), rr.get("algorithmic_bytes_per_codeword_iteration")
+        return t / a if (t and a) else None
+
+    comp["C2_R1.3"] = _companion(out.get("amp_r13"), cpu_match=_bm(out.get("amp_r13"), "identical_section_decisions"))
+    comp["C2_f64"] = _companion(out.get("amp_f64"), cpu_match=_bm(out.get("amp_f64"), "identical_section_decisions"))
+    bp = out.get("bp")
+    if bp:
+        bh = bp.get("roofline_hbm") or {}
+        comp["C3"] = _companion(bp, traffic_ratio=(bh["traffic"] / bh["algorithmic_bytes_per_codeword_iteration"])
+                                if bh.get("traffic") else None,
+                                cpu_match=_bm(bp, "identical_codeword_decisions"))
+    for i, o in enumerate(out.get("bp_ebn0") or []):
+        comp["C3_%sdB" % o.get("ebn0", i)] = _companion(o, cpu_match=_bm(o, "identical_decisions_where_cpu_decodes"))
+    for o, name in zip(out.get("bp_variants") or [], ("C3_sumprod2_f64", "C3_r56")):
+        comp[name] = _companion(o, cpu_match=_bm(o, "identical_decisions_where_cpu_decodes"))
+    for k, name in (("sc", "C4"), ("sc_notebook", "C4_notebook")):
+        if out.get(k):
+            comp[name] = _companion(out[k], traffic_ratio=tratio(out[k]),
+                                    cpu_match=_bm(out[k], "identical_section_decisions"))
+    cc = out.get("concat")
+    if cc:
+        cr = cc.get("roofline") or {}
+        a_bytes = 4.0 * (cc.get("n") or 0) * 1024 * 512  # one pass over the f32 design matrix
+        comp["C5"] = _companion(cc, traffic_ratio=cr["traffic"] / a_bytes if (cr.get("traffic") and a_bytes) else None,
+                                cpu_match=(cc.get("decision_match") or {}).get(
+                                    "identical_block_decisions_where_oracle_decodes"))
+    line["companions"] = {k: v for k, v in comp.items() if v is not None}
+    line["detail"] = detail_rel
+    return line
+
+
+def write_detail(out, detail_dir):
+    """Full per-configuration detail (kernel times, CPU samples, notes) as
+    <detail_dir>/bench_detail_<libsha>.json; returns the repo-relative path."""
+    d = detail_dir if os.path.isabs(detail_dir) else os.path.join(REPO, detail_dir)
+    path = os.path.join(d, f"bench_detail_{lib_digest()}.json")
+    try:
+        os.makedirs(d, exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+    except OSError as e:
+        sys.stderr.write(f"bench.py: could not write {path}: {e}\n")
+    return os.path.relpath(path, REPO)
 
 
 def main():
@@ -1128,9 +1264,15 @@ def main():
         out["cpu_baseline"] = amp_cpu_baseline(st, args, args.cpu_seconds, procs)
         if not args.no_bp:
             out["bp"]["cpu_baseline"] = bp_cpu_baseline(bst, 0.4 * args.cpu_seconds, procs)
-    out["summary"] = summary(out)  # last key: inside the tail of the line a log keeps
+    out["summary"] = summary(out)
     if d.rank == 0:
-        print(json.dumps(out), flush=True)
+        line = compact_line(out, write_detail(out, args.detail_dir))
+        s = json.dumps(line, separators=(",", ":"))
+        if len(s) >= LINE_MAX_BYTES:  # never print a line the driver cannot ingest
+            sys.stderr.write(f"bench.py: line of {len(s)} B; dropping companions\n")
+            line["companions"] = {k: {"value": v["value"]} for k, v in line["companions"].items()}
+            s = json.dumps(line, separators=(",", ":"))
+        print(s, flush=True)
     if comm is not None:
         comm.destroy()
     d.close()

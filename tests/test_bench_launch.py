@@ -183,3 +183,33 @@ def test_pmc_files_only_for_this_build(tmp_path, monkeypatch):
     (prof / "r09_pmc_sq_bench.json").write_text(json.dumps({"lib_sha256": dig, "amp": {
         "valu_wave_insts_per_codeword_iteration": 5.0}}))
     assert b.pmc_sq("amp")[0]["valu_wave_insts_per_codeword_iteration"] == 5.0
+
+
+def test_compact_line_fits_the_driver(tmp_path):
+    """The printed line is built from the full record (here round 5's, whose
+    23 KB line the driver could not ingest): under 8 KB, with the contract keys,
+    the C2 roofline and cpu_baseline, and one short entry per companion."""
+    b = _bench_module()
+    with open(os.path.join(REPO, "tests", "data", "bench_out_r05.json")) as f:
+        out = json.load(f)
+    line = b.compact_line(out, "profiles/bench_detail_0123456789abcdef.json")
+    s = json.dumps(line, separators=(",", ":"))
+    assert len(s) < b.LINE_MAX_BYTES and len(s) < 4096, len(s)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "dtype", "config",
+              "roofline", "cpu_baseline", "higher_is_better", "scaling", "vs_baseline", "data"):
+        assert k in line, k
+    rf = line["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "valu_issue_frac", "lds_bank_conflict_frac"):
+        assert rf[k] is not None, k
+    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    cb = line["cpu_baseline"]
+    for k in ("value", "unit", "cores", "kind", "sample", "port_over_reference_speed", "ber_match"):
+        assert cb[k] is not None, k
+    comp = line["companions"]
+    for k in ("C2_R1.3", "C2_f64", "C3", "C4", "C4_notebook", "C5"):
+        assert k in comp and len(json.dumps(comp[k])) <= 150, (k, comp.get(k))
+    assert line["value"] == out["value"] and line["ms_per_step"] == out["ms_per_step"]
+    assert line["detail"].startswith("profiles/bench_detail_")
+    # the detail file holds the full record
+    p = b.write_detail(out, str(tmp_path))
+    assert json.load(open(os.path.join(REPO, p))) == out
