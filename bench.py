@@ -625,12 +625,13 @@ def bp_variant(args, d, std, rate, z, dectype, prec, ebn0, B, steps, max_it=50, 
            "value": d.world * B * steps / el, "unit": "codewords/s", "batch_per_gpu": B, "ebn0": ebn0,
            "avg_executed_iterations": float(np.where(its < max_it, its + 1, max_it).mean()),
            "frame_errors": fe, "kernel_ms_per_launch": ph.get("bp_flood", (0.0, 1))[0] / max(ph.get("bp_flood", (0, 1))[1], 1)}
-    if prec == _native.SG_F32 and out["kernel_ms_per_launch"] > 0:  # LDS bound, as the C3 line
+    kname = c.decode_kernel(dectype, prec)
+    if kname.startswith("bp_grouped") and out["kernel_ms_per_launch"] > 0:  # messages in LDS: the C3 bound
         cwit = float(np.where(its < max_it, its + 1, max_it).sum())
         lach = 16 * c.Nmsg * cwit / (out["kernel_ms_per_launch"] * 1e-3) / 1e9
         lpk = bp_lds_peak_gbs(_native.cu_count())
         out["roofline"] = {"bound": "lds", "achieved": lach, "peak": lpk, "unit": "GB/s", "frac": lach / lpk,
-                           "kernel": c.decode_kernel(dectype, prec)}
+                           "kernel": kname}
     if cpu_seconds > 0:
         from oracle import cpu_pool
         capp, cit, done, cel = cpu_pool.bp_decode(procs, dectype, ch, c.vdeg, c.cdeg, c.intrlv, max_it, 0.7,

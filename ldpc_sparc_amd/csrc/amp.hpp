@@ -274,6 +274,15 @@ struct Cw2dTables {
 };
 int cw2d_launch_iter(const Cw2dTables &tb, const RegBufs<double> &bf, const AmpScalars &sc, const AmpParams &pr,
                      int t, hipStream_t s);
+// The compile-time bounds of amp_cw2d.hip, checked by the plan builder (build_regular: a plan outside them keeps
+// the staged engine) and again by cw2d_launch_iter: P = 8192 (N2 = 8192 Q), an even Q <= 64, one column block,
+// L <= 1024 and a multiple of 4 (statistics workgroups), M <= 512 (one wavefront of 8 entries per lane per
+// section), class slices of at most CW2_SLICE entries, 12, 13, 14 or 16 outputs per thread.
+inline bool cw2d_supported(const Cw2dTables &tb) {
+    return tb.Q % 2 == 0 && tb.Q > 0 && tb.Q <= 64 && tb.L > 0 && tb.L <= 1024 && tb.L % 4 == 0 &&
+           tb.Lblk == tb.L && tb.maxcls <= CW2_SLICE && tb.M > 0 && tb.M <= 512 && tb.N2 == 8192 * tb.Q &&
+           (tb.OT == 12 || tb.OT == 13 || tb.OT == 14 || tb.OT == 16);
+}
 int cw_launch_iter(const CwTables &tb, const RegBufs<float> &bf, const AmpScalars &sc, const AmpParams &pr, int t,
                    hipStream_t s);
 

@@ -757,7 +757,7 @@ __global__ __launch_bounds__(64 * ST_WAVES) void cw2d_stats(Cw2dTables tb, RegBu
         double err = ss;
         if (bf.true_idx) {
             const double st = s[tb.qpos[l * tb.M + bf.true_idx[lb + l]]];
-            err = ss - 2.0 * (exp(st / tau - M / tau) * inv) + 1.0;
+            err = ss - 2.0 * (exp(d_arg(st, ms, tau, inv_tau)) * inv) + 1.0;  // as the entries (and sm_arg)
         }
         tb.sec[(lb + l) * 2] = ss;
         tb.sec[(lb + l) * 2 + 1] = err;
@@ -845,10 +845,8 @@ static int cw2d_launch(const Cw2dTables &tb, const RegBufs<double> &bf, const Am
 int cw2d_launch_iter(const Cw2dTables &tb, const RegBufs<double> &bf, const AmpScalars &sc, const AmpParams &pr,
                      int t, hipStream_t s) {
     if (bf.B <= 0) return SG_OK;
-    if (tb.Q % 2 || tb.Q > 64 || tb.L > 1024 || tb.L % ST_WAVES_MIN || tb.Lblk != tb.L || tb.maxcls > CW2_SLICE ||
-        tb.M > 64 * ST_K ||
-        tb.N2 != D_P * tb.Q || tb.M <= 0)
-        return fail(SG_ERR_UNSUPPORTED, "f64 split engine: sizes outside its compile-time bounds");
+    static_assert(D_P == 8192 && ST_WAVES_MIN == 4 && 64 * ST_K == 512, "cw2d_supported (amp.hpp) states these");
+    if (!cw2d_supported(tb)) return fail(SG_ERR_UNSUPPORTED, "f64 split engine: sizes outside its compile-time bounds");
     ProfScope ps(SG_PH_AMP_CW, s);
     switch (tb.OT) {
     case 12: SG_TRY(cw2d_launch<12>(tb, bf, sc, pr, t, s)); break;

@@ -785,6 +785,8 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
 // Tables of the regular engine (amp_fused.hip), one transform per column
 // block: class order of each block's entries and the needed-row structure of
 // the two FFT stages.  Sizes: P = stage-1 FFT length (LDS resident), Q = N2/P.
+static Cw2dTables c2dtables(const sg_amp_plan *p);
+
 static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t *order1,
                          const std::vector<double> &t_scale) {
     const long long N = p->w, N2 = p->N2;
@@ -1024,7 +1026,7 @@ static int build_regular(sg_amp_plan *p, const uint32_t *order0, const uint32_t 
     if (p->precision == SG_F64 && nT == 1 && P == (1 << 13) && Lblk <= 2 * CW2_THREADS && p->L <= 1024 &&
         p->L % 4 == 0 && M <= 512 && Q % 2 == 0 && Q <= 64 && p->rmaxcls <= CW2_SLICE && !p->no_cw) {
         SG_TRY(build_cw2(p, order0, t_scale[0], row_k1[0], cls_ptr, cls_ls));
-        p->cw = p->cw2OT != 0;
+        p->cw = p->cw2OT != 0 && cw2d_supported(c2dtables(p));  // else the staged engine, never a decode-time error
     }
     return SG_OK;
 }

@@ -1,6 +1,8 @@
 // C ABI of the LDPC decoder: graph upload, batched decode, reference-compatible
 // scalar shims (ldpc.py:463-503 ctypes targets).
 #include <algorithm>
+#include <cfloat>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -375,11 +377,16 @@ static int decode_host(sg_graph *g, int dectype, int precision, const double *ch
         std::vector<float> tmp(n);
         bool nonfinite = false;
         for (size_t i = 0; i < n; ++i) {
-            tmp[i] = (float)ch[i];
-            nonfinite |= !std::isfinite(tmp[i]);
+            const double v = ch[i];
+            if (std::isfinite(v)) {  // a finite double past float's range stays finite: +-FLT_MAX
+                tmp[i] = (float)std::min(std::max(v, -(double)FLT_MAX), (double)FLT_MAX);
+            } else {
+                tmp[i] = (float)v;
+                nonfinite = true;
+            }
         }
-        // a NaN or infinite input (or one that overflows float) goes to the table kernel: NaN and
-        // inf semantics of the reference; the grouped kernel saturates channel LLRs at +-1e30
+        // a NaN or infinite input goes to the table kernel: NaN and inf semantics of the reference; finite
+        // inputs (clamped to +-FLT_MAX above) take the grouped kernel, which saturates channel LLRs at +-1e30
         ch_has_nan = nonfinite;
         SG_HIP(hipMemcpyAsync(g->d_ch, tmp.data(), n * sizeof(float), hipMemcpyHostToDevice, s));
         SG_HIP(hipStreamSynchronize(s));

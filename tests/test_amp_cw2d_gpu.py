@@ -90,13 +90,16 @@ def test_f64_split_engine_vs_oracle(monkeypatch):
 
 
 def test_f64_shipped_choice_full_batch(monkeypatch):
-    """B = 256 (the bench batch) with the automatic choice: the split engine,
-    handing over to the staged engine once half the batch has stopped; same
+    """B = 256 (the bench batch size) with the automatic choice: the split
+    engine, handing over to the staged engine once half the batch has stopped
+    (R = 1.3: codewords stop after 14-18 iterations, so the hand-over fires; at
+    R = 1.5 nearly every codeword runs to t_max and none happens); same
     decisions and stopping iterations as the staged engine throughout."""
-    op, true, Y = _batch(1024, 512, 1.5, 256, 11, 3)
+    op, true, Y = _batch(1024, 512, 1.3, 256, 11, 3)
     (ma, ta, na, _), ia = _decode(monkeypatch, op, Y, true, None)
     (mb, tb, nb, _), ib = _decode(monkeypatch, op, Y, true, "staged")
     assert ia["engine"] == 2 and ib["engine"] == 1
+    assert ia["handover_iter"] > 0  # the split -> staged state transfer ran (class-order s, stM / stI, z, tau, phi)
     assert np.array_equal(ta, tb)
     assert np.array_equal(ma, mb)
     np.testing.assert_allclose(na, nb, rtol=0, atol=1e-9)

@@ -570,26 +570,30 @@ def _c2_batch(seed_design, seed_data, B, R):
     return W, L, M, n, o0, o1, op, true, Y
 
 
-def _bench_c2_batch(R, seed=1, B=256):
+def _bench_c2_batch(R, seed=1, B=256, prec=None):
     """The received words bench.py times (bench.amp_setup: design seed 0,
-    Philox seed 1 stream 0, encode and AWGN on the GPU), downloaded."""
+    Philox seed 1 stream 0, encode and AWGN on the GPU, in the line's
+    precision), downloaded."""
     L, M, logM = 1024, 512, 9
     n = int(round(L * logM / R))
     W = np.array(15.0)
+    prec = _native.SG_F32 if prec is None else prec
+    dt = np.float32 if prec == _native.SG_F32 else np.float64
+    es = np.dtype(dt).itemsize
     o0, o1 = sparc.generate_ordering(W, n, L * M, 0)
     op = sparc.DesignOperator(W, L, M, n, o0, o1)
-    plan = op.plan(_native.SG_F32)
+    plan = op.plan(prec)
     lib = _native.lib()
     d_bits = _native.DeviceBuffer(B * L * logM)
     d_true = _native.DeviceBuffer(B * L * 4)
-    d_x = _native.DeviceBuffer(B * n * 4)
-    d_y = _native.DeviceBuffer(B * n * 4)
+    d_x = _native.DeviceBuffer(B * n * es)
+    d_y = _native.DeviceBuffer(B * n * es)
     _native.check(lib.sg_rng_bits_device(seed, 0, B, L * logM, d_bits.ptr, None))
     _native.check(lib.sg_bits_to_sections_device(d_bits.ptr, B, L, logM, d_true.ptr, None))
     _native.check(lib.sg_amp_encode_device(plan, d_true.ptr, B, d_x.ptr, None))
-    _native.check(lib.sg_awgn_device(_native.SG_F32, seed, 0, d_x.ptr, B, n, 1.0, d_y.ptr, None))
+    _native.check(lib.sg_awgn_device(prec, seed, 0, d_x.ptr, B, n, 1.0, d_y.ptr, None))
     _native.synchronize()
-    Y = d_y.download(np.zeros((B, n), np.float32)).astype(np.float64)
+    Y = d_y.download(np.zeros((B, n), dt)).astype(np.float64)
     true = d_true.download(np.zeros((B, L), np.int32))
     return W, L, M, n, o0, o1, op, true, Y
 
@@ -668,6 +672,37 @@ def test_shipped_c2_batch_vs_oracle(monkeypatch, R, inputs):
     assert abs(cb - gb) <= 3 * np.sqrt(max(cb, 1.0 / nb) * (1 - cb) / nb) + 1.0 / nb, (cb, gb)
     if R == 1.3:  # decodable rate: most codewords decode, on both sides
         assert np.mean([np.array_equal(res[b][0], true[b]) for b in range(B)]) >= 0.75
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [1.5, 1.3])
+def test_shipped_f64_c2_batch_vs_oracle(monkeypatch, R):
+    """The bench's double-precision C2 line (bench.amp_f64: the bench's Philox
+    batch generated in float64, B = 256, automatic engine choice: the f64 split
+    engine amp_cw2d.hip, handing over to the staged engine once half the batch
+    has stopped) against the CPU restatement of sparc.py:883-999 (float128
+    softmax) on ALL 256 codewords.  f64 bar (DESIGN.md "AMP, f64"): identical
+    t_final and MAP decisions on every codeword, NMSE within 1e-8 at every
+    iteration (the restatement's softmax is float128, the engine's float64)."""
+    from oracle import cpu_pool
+    monkeypatch.delenv("SG_AMP_ENGINE", raising=False)
+    monkeypatch.delenv("SG_AMP_HANDOVER", raising=False)
+    B = 256
+    W, L, M, n, o0, o1, op, true, Y = _bench_c2_batch(R, prec=_native.SG_F64)
+    plan = op.plan(_native.SG_F64)
+    assert _native.lib().sg_amp_plan_engine(plan, B) == 2
+    mi, tf, nm, _ = sparc.amp_decode_batch(Y, op, 1.0, 25, true_idx=true, precision=_native.SG_F64)
+    last = _native.amp_last_decode(plan)
+    assert last["engine"] == 2
+    res, _ = cpu_pool.amp_decode(cpu_pool.host_cores(16), W, L, M, n, o0, o1, Y, true, 25)
+    assert sorted(res) == list(range(B))
+    for b in range(B):
+        cm, ct_, cn, _ = res[b]
+        assert int(tf[b]) == ct_, (b, tf[b], ct_)
+        assert np.array_equal(mi[b], cm), (b, np.mean(mi[b] != cm))
+        np.testing.assert_allclose(nm[b, :, 0], cn, rtol=0, atol=1e-8)
+    if R == 1.3:
+        assert np.mean((mi == true).all(1)) >= 0.75
 
 
 @pytest.mark.gpu

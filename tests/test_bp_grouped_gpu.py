@@ -129,12 +129,12 @@ def test_graphs_outside_the_grouped_layout_take_the_table_kernel():
         _graph(vdeg, cdeg, intrlv)
 
 
-@pytest.mark.parametrize("bad", [np.nan, np.inf, -np.inf, 1e300])
+@pytest.mark.parametrize("bad", [np.nan, np.inf, -np.inf])
 def test_nonfinite_channel_input_takes_the_table_kernel(monkeypatch, bad):
     """The grouped kernel has no NaN semantics (built -fno-honor-nans) and
-    saturates channel LLRs at +-1e30: a host batch holding a NaN, an infinity
-    (a hard-known bit) or a double that overflows float decodes through the
-    table kernel, so its results equal the table kernel's."""
+    saturates channel LLRs at +-1e30: a host batch holding a NaN or an infinity
+    (a hard-known bit) decodes through the table kernel, so its results equal
+    the table kernel's."""
     c = code("802.11n", "1/2", 27)
     ch = _awgn(c, 1.5, 8, np.random.default_rng(4))
     ch[3, 17] = bad
@@ -147,6 +147,34 @@ def test_nonfinite_channel_input_takes_the_table_kernel(monkeypatch, bad):
         monkeypatch.setenv("SG_BP_GROUPED", "0")
         tapp, tit = _decode(g, ch, 20, 0.7)
         assert np.array_equal(it, tit) and np.array_equal(app.view(np.uint32), tapp.view(np.uint32))
+    finally:
+        _native.lib().sg_ldpc_graph_destroy(g)
+
+
+def test_overflowing_channel_input_stays_finite(monkeypatch):
+    """A finite double past float's range (1e300) is a finite LLR for the
+    reference (c_ldpc.c computes in double).  The f32 host path clamps it to
+    +-FLT_MAX and decodes it through the grouped kernel, which saturates large
+    channel LLRs at +-1e30: the results equal the same batch with +-1e30 in its
+    place, hold no NaN, and take the float64 oracle's decisions on every
+    codeword the oracle decodes."""
+    c = code("802.11n", "1/2", 27)
+    ch = _awgn(c, 2.0, 8, np.random.default_rng(4))
+    ch[3, 17], ch[5, 3], ch[5, 4] = 1e300, -1e300, 1e300
+    sat = ch.copy()
+    sat[np.abs(sat) > 1e30] = np.sign(sat[np.abs(sat) > 1e30]) * 1e30
+    vdeg, cdeg, intrlv = (np.asarray(a, np.int64) for a in (c.vdeg, c.cdeg, c.intrlv))
+    g = _graph(vdeg, cdeg, intrlv)
+    try:
+        monkeypatch.setenv("SG_BP_GROUPED", "1")
+        app, it = _decode(g, ch, 20, 0.7)
+        sapp, sit = _decode(g, sat, 20, 0.7)
+        assert np.isfinite(app).all()
+        assert np.array_equal(it, sit) and np.array_equal(app.view(np.uint32), sapp.view(np.uint32))
+        oapp, oit = bp.decode_batch("minsum", ch, vdeg, cdeg, intrlv, 20, 0.7)
+        dec = oit < 20
+        assert dec.any()
+        assert np.array_equal((app < 0)[dec], (oapp < 0)[dec]) and np.array_equal(it[dec], oit[dec])
     finally:
         _native.lib().sg_ldpc_graph_destroy(g)
 
