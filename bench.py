@@ -34,15 +34,16 @@ received words the GPU decoded, bounded in time (rank 0, N=1 only).  The
 decisions of both are compared over the whole sample.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-       N>1 without torch.distributed.run's environment: bench.py starts
-       torch.distributed.run itself (one process per GPU) before touching the
-       GPU, and exits non-zero when fewer than N GPUs are visible.
+       N>1 without a launcher's environment: bench.py starts its N ranks
+       itself (ldpc_sparc_amd.launch, one process per GPU, no PyTorch) before
+       touching the GPU, and exits non-zero when fewer than N GPUs are
+       visible; under torch.distributed.run the ranks meet the same way
+       (ldpc_sparc_amd.rendezvous).
 """
 import argparse
 import json
 import os
 import socket
-import subprocess
 import sys
 import time
 
@@ -184,9 +185,10 @@ def visible_gpus():
 
 
 def maybe_spawn(args):
-    """--gpus N > 1 outside torch.distributed.run: start it (one rank per GPU)
-    as a child process and exit with its code.  Nothing here touches the GPU,
-    so the parent never holds GPU state while the ranks run."""
+    """--gpus N > 1 outside a launcher's environment: start N ranks of this
+    script (ldpc_sparc_amd.launch, one process per GPU, no PyTorch) as child
+    processes and exit with the job's code.  Nothing here touches the GPU, so
+    the parent never holds GPU state while the ranks run."""
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is not None:
         if int(world_env) != args.gpus:
@@ -201,93 +203,59 @@ def maybe_spawn(args):
             sys.stderr.write(f"bench.py: --gpus {args.gpus} but only {ng} GPU(s) visible; refusing to run "
                              f"fewer ranks\n")
             sys.exit(2)
-    with socket.socket() as so:
-        so.bind(("127.0.0.1", 0))
-        port = so.getsockname()[1]
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
-    sys.exit(subprocess.run(cmd, env=env).returncode)
+    from ldpc_sparc_amd import launch
+    sys.exit(launch.spawn(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
 
 
 def rendezvous_check(d):
     """--rendezvous-check: every rank joins, barriers, and reports its rank;
     rank 0 prints the ranks that joined (CPU only, no GPU call)."""
-    ranks = [d.rank]
-    if d.world > 1:
-        obj = [None] * d.world
-        d.dist.all_gather_object(obj, d.rank)
-        ranks = obj
+    ranks = d.group.allgather_obj(d.rank) if d.world > 1 else [d.rank]
     d.barrier()
     if d.rank == 0:
         print(json.dumps({"rendezvous": "ok", "n_ranks": len(ranks), "ranks": sorted(ranks),
-                          "world_size": d.world}), flush=True)
+                          "world_size": d.world, "torch_loaded": "torch" in sys.modules}), flush=True)
     d.close()
 
 
 class Dist:
-    """torch.distributed (gloo, CPU only) for rendezvous, barriers and the
-    RCCL unique id; all GPU work goes through libldpc_sparc_amd."""
+    """The ranks of this job (ldpc_sparc_amd.rendezvous: standard-library TCP on
+    the node) for rendezvous, barriers and the RCCL unique id; all GPU work,
+    the counter all-reduce included, goes through libldpc_sparc_amd."""
 
     def __init__(self):
+        from ldpc_sparc_amd.rendezvous import HostGroup
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
-        self.pg = None
-        if self.world > 1:
-            import torch.distributed as dist
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            # gloo prints its peer-connection notice on stdout: keep stdout for
-            # the one JSON line (the notice goes to stderr)
-            sys.stdout.flush()
-            saved = os.dup(1)
-            os.dup2(2, 1)
-            try:
-                dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
-                dist.barrier()
-            finally:
-                sys.stdout.flush()
-                os.dup2(saved, 1)
-                os.close(saved)
-            self.dist = dist
+        self.group = HostGroup(self.rank, self.world) if self.world > 1 else None
 
     def barrier(self):
-        if self.world > 1:
-            self.dist.barrier()
+        if self.group is not None:
+            self.group.barrier()
 
     def max(self, x):
-        if self.world == 1:
-            return x
-        import torch
-        t = torch.tensor([float(x)], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t.item())
+        return x if self.group is None else self.group.max(x)
 
     def bcast_bytes(self, b):
-        if self.world == 1:
-            return b
-        obj = [b]
-        self.dist.broadcast_object_list(obj, src=0)
-        return obj[0]
+        return b if self.group is None else self.group.bcast_bytes(b if self.rank == 0 else b"")
 
     def close(self):
-        if self.world > 1:
-            self.dist.destroy_process_group()
+        if self.group is not None:
+            self.group.barrier()
+            self.group.close()
 
 
 class HostCounterComm:
-    """Counter all-reduce through gloo on the host: only for rehearsals in which
-    several ranks share one GPU (RCCL needs one GPU per rank)."""
+    """Counter all-reduce through the host rendezvous group: only for
+    rehearsals in which several ranks share one GPU (RCCL needs one GPU per rank)."""
 
     def __init__(self, d):
         self.d = d
 
     def allreduce_sum_i64(self, dbuf, count):
-        import torch
         v = dbuf.download(np.zeros(count, np.int64))
-        t = torch.from_numpy(v)
-        self.d.dist.all_reduce(t)
-        dbuf.upload(t.numpy())
+        dbuf.upload(self.d.group.allreduce_sum_i64(v))
 
     def destroy(self):
         pass
@@ -1037,7 +1005,7 @@ def write_detail(out, detail_dir):
 def main():
     args = parse()
     guard_env()
-    maybe_spawn(args)  # --gpus N > 1 outside torch.distributed.run: re-launched as N ranks, exits
+    maybe_spawn(args)  # --gpus N > 1 outside a launcher: re-launched as N ranks, exits
     d = Dist()
     if args.rendezvous_check:
         return rendezvous_check(d)
@@ -1053,15 +1021,13 @@ def main():
     rccl_ranks = 1
     if d.world > 1:
         if d.world > ndev:
-            comm, counter_path = HostCounterComm(d), "gloo (BENCH_REHEARSAL: ranks share a GPU)"
+            comm, counter_path = HostCounterComm(d), "host (BENCH_REHEARSAL: ranks share a GPU)"
         else:
             uid = d.bcast_bytes(_native.Comm.unique_id() if d.rank == 0 else None)
             comm, counter_path = _native.Comm(d.world, d.rank, uid), "rccl"
             rccl_ranks, dev = comm.info()
             # every rank on its own GPU: count the distinct (host, device) pairs
-            import torch
-            obj = [None] * d.world
-            d.dist.all_gather_object(obj, (socket.gethostname(), dev))
+            obj = [tuple(x) for x in d.group.allgather_obj([socket.gethostname(), dev])]
             if len(set(obj)) != d.world or rccl_ranks != d.world:
                 sys.stderr.write(f"bench.py: RCCL sees {rccl_ranks} ranks on {len(set(obj))} distinct GPUs, "
                                  f"expected {d.world}\n")

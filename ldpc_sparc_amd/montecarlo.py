@@ -6,7 +6,8 @@ Here one process per GPU runs a campaign together: every SNR point is split
 into fixed blocks of codewords, block b being seeded by (seed, point, b) so
 that the result does not depend on how many GPUs took part; each round the
 blocks are dealt to ranks by contiguous ranges, and ONE all-reduce of an int64
-counter vector (RCCL over xGMI between GPUs, or gloo for CPU tests) gives every
+counter vector (RCCL over xGMI between GPUs, or the host rendezvous group of
+rendezvous.py for CPU tests) gives every
 rank the global counts that drive the stopping rule.
 
 Counters per point: [units, bit_errors, frame_errors, aux0, aux1] where aux
@@ -33,26 +34,24 @@ def shard_range(total, rank, world):
 
 
 class Aggregator:
-    """Sum of int64 counter vectors over the ranks of a campaign."""
+    """Sum of int64 counter vectors over the ranks of a campaign: RCCL between
+    GPUs (`comm`, a `_native.Comm`), or the host rendezvous group for CPU
+    rehearsals (`group`, a `rendezvous.HostGroup`)."""
 
-    def __init__(self, backend="none", comm=None):
-        assert backend in ("none", "gloo", "rccl")
+    def __init__(self, backend="none", comm=None, group=None):
+        assert backend in ("none", "host", "rccl")
+        assert backend != "host" or group is not None, "the host backend needs a rendezvous group"
         self.backend = backend
         self.comm = comm
+        self.group = group
         self._dbuf = None
-        if backend == "gloo":
-            import torch.distributed as dist
-            self.dist = dist
 
     def allreduce(self, counts):
         counts = np.ascontiguousarray(counts, dtype=np.int64)
         if self.backend == "none":
             return counts.copy()
-        if self.backend == "gloo":
-            import torch
-            t = torch.from_numpy(counts.copy())
-            self.dist.all_reduce(t)
-            return t.numpy().astype(np.int64)
+        if self.backend == "host":
+            return self.group.allreduce_sum_i64(counts)
         if self._dbuf is None or self._dbuf.nbytes < counts.nbytes:
             self._dbuf = _native.DeviceBuffer(counts.nbytes)
         self._dbuf.upload(counts)

@@ -1,5 +1,5 @@
-"""CPU tests of bench.py's launcher (no GPU): --gpus N starts N ranks through
-torch.distributed.run before any GPU call (the reference's own parallelism is
+"""CPU tests of bench.py's launcher (no GPU): --gpus N starts N ranks
+(ldpc_sparc_amd.launch, no PyTorch) before any GPU call (the reference's own parallelism is
 one process per sim_id, ldpc_jossy/py/ldpc_awgn.py:125-131), a mismatched
 WORLD_SIZE or engine knobs in the environment are refused, and the CPU
 baseline pool (oracle/cpu_pool.py) decodes like the serial restatement."""
@@ -64,9 +64,18 @@ fake.amdsmi_get_processor_handles = lambda: list(range(8))
 fake.amdsmi_shut_down = lambda: None
 sys.modules["amdsmi"] = fake
 calls = []
-class _R:
-    returncode = 0
-subprocess.run = lambda cmd, env=None: (calls.append(cmd), _R())[1]
+class _P:
+    def __init__(self, cmd, env=None):
+        calls.append((cmd, {k: env[k] for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "SG_RDZV_PORT")}))
+    def poll(self):
+        return 0
+    def send_signal(self, s):
+        pass
+    def kill(self):
+        pass
+    def wait(self):
+        return 0
+subprocess.Popen = _P
 sys.argv = ["bench.py", "--gpus", "8"]
 import bench
 code = None
@@ -77,22 +86,26 @@ except SystemExit as e:
 import json
 print(json.dumps({"code": code, "torch_loaded": "torch" in sys.modules,
                   "hip_loaded": any("amdhip" in l for l in open("/proc/self/maps")),
-                  "cmd": calls[0] if calls else None}))
+                  "calls": calls}))
 '''
 
 
 def test_launcher_counts_gpus_without_hip():
-    """--gpus 8 with 8 GPUs visible (amdsmi stubbed): the parent starts
-    torch.distributed.run with 8 processes per node and exits with its code,
-    without importing torch or mapping the HIP runtime (so no GPU call can
-    precede the launch)."""
+    """--gpus 8 with 8 GPUs visible (amdsmi stubbed): the parent starts 8 ranks
+    of bench.py (ldpc_sparc_amd.launch: RANK 0..7, one rendezvous port) and
+    exits with the job's code, without importing torch or mapping the HIP
+    runtime (so no GPU call can precede the launch)."""
     env = {k: v for k, v in _env().items() if not k.endswith("_VISIBLE_DEVICES")}
     r = subprocess.run([sys.executable, "-c", _LAUNCH_PROBE], env=env, capture_output=True, text=True,
                        timeout=120, cwd=REPO)
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["code"] == 0 and not out["torch_loaded"] and not out["hip_loaded"], out
-    assert "torch.distributed.run" in out["cmd"] and "--nproc-per-node=8" in out["cmd"]
+    assert len(out["calls"]) == 8
+    assert [c[1]["RANK"] for c in out["calls"]] == [str(r) for r in range(8)]
+    assert all(c[1]["WORLD_SIZE"] == "8" for c in out["calls"])
+    assert len({c[1]["SG_RDZV_PORT"] for c in out["calls"]}) == 1
+    assert all(c[0][1].endswith("bench.py") and "--gpus" in c[0] for c in out["calls"])
 
 
 def test_visible_devices_mask_narrows_count():
@@ -100,7 +113,48 @@ def test_visible_devices_mask_narrows_count():
                        capture_output=True, text=True, timeout=120, cwd=REPO)
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
-    assert out["code"] == 2 and out["cmd"] is None, out
+    assert out["code"] == 2 and out["calls"] == [], out
+
+
+def _no_torch_env(tmp_path):
+    """An environment in which `import torch` fails (a stub package first on
+    PYTHONPATH): the multi-rank paths must not need PyTorch (north_star)."""
+    stub = tmp_path / "notorch" / "torch"
+    stub.mkdir(parents=True)
+    (stub / "__init__.py").write_text("raise ImportError('torch is blocked in this test')\n")
+    env = _env()
+    env["PYTHONPATH"] = str(tmp_path / "notorch") + os.pathsep + env.get("PYTHONPATH", "")
+    return env
+
+
+def test_rendezvous_without_torch(tmp_path):
+    """--gpus 4 --rendezvous-check with torch not importable: four ranks
+    started by the stdlib launcher meet over the stdlib rendezvous."""
+    env = _no_torch_env(tmp_path)
+    chk = subprocess.run([sys.executable, "-c", "import torch"], env=env, capture_output=True, text=True)
+    assert chk.returncode != 0 and "blocked" in chk.stderr
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "4", "--rendezvous-check"], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert out["ranks"] == [0, 1, 2, 3] and out["torch_loaded"] is False
+
+
+def test_rendezvous_under_torchrun_file_discovery():
+    """The driver launches N > 1 through torch.distributed.run, whose agent
+    holds MASTER_PORT: the ranks then find rank 0's relay through the temp
+    file keyed by the run (no SG_RDZV_PORT)."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", BENCH, "--gpus", "3", "--rendezvous-check"]
+    env = {k: v for k, v in _env().items() if k != "SG_RDZV_PORT"}
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert out["ranks"] == [0, 1, 2]
 
 
 def test_cpu_pool_matches_serial_oracle():

@@ -1,6 +1,6 @@
 """CPU tests of the multi-GPU Monte-Carlo layer (montecarlo.py): sharding,
-the counter all-reduce (gloo, world_size 2, the same code path that uses RCCL
-between GPUs), invariance of a campaign's result to the number of ranks,
+the counter all-reduce (the stdlib host rendezvous group, world_size 2, the
+same code path that uses RCCL between GPUs), invariance of a campaign's result to the number of ranks,
 checkpoint/resume, and the results.txt -> CSV conversion of results2csv.c."""
 import json
 import os
@@ -8,7 +8,7 @@ import socket
 
 import numpy as np
 import pytest
-import torch.multiprocessing as mp
+import multiprocessing as mp
 
 from ldpc_sparc_amd import montecarlo as mc
 
@@ -87,11 +87,9 @@ def sequential_sim(trial, min_errors, max_blocks, block, n_points, snr0, p_step)
 
 
 def _worker(rank, world, port, q, ckpt):
-    import torch.distributed as dist
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    agg = mc.Aggregator("gloo")
+    from ldpc_sparc_amd.rendezvous import HostGroup
+    group = HostGroup(rank, world, "127.0.0.1", port)
+    agg = mc.Aggregator("host", group=group)
     res = []
     for pt in range(3):
         res.append(mc.run_point(fake_trial, pt, block=64, blocks_per_round=5, rank=rank, world=world, agg=agg,
@@ -100,7 +98,8 @@ def _worker(rank, world, port, q, ckpt):
     camp = mc.ldpc_awgn_campaign("802.11n", "1/2", 27, rank=rank, world=world, agg=agg, N_MEASUREMENTS=4,
                                  MIN_ERRORS=37, MAX_BLOCKS=3000, block=32, blocks_per_round=3, trial=FakeUnitTrial())
     q.put((rank, res, s, camp))
-    dist.destroy_process_group()
+    group.barrier()
+    group.close()
 
 
 def _run(world, ckpt=None):
@@ -181,9 +180,9 @@ def test_results_csv_format():
     assert mc.results_to_csv([line]) == ["16, 0.666667, 1, 3, -1.31038, 100, 100, 4800, 1439, 20000"]
 
 
-def _c5_rehearsal(world, ckpt, extra=()):
-    """tools/c5_sweep.py --rehearsal at `world` ranks (torch.distributed.run,
-    gloo on the CPU); the JSON lines rank 0 prints."""
+def _c5_rehearsal(world, ckpt, extra=(), env=None):
+    """tools/c5_sweep.py --rehearsal at `world` ranks (ldpc_sparc_amd.launch,
+    the host rendezvous group on the CPU); the JSON lines rank 0 prints."""
     import subprocess
     import sys
     tool = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "c5_sweep.py")
@@ -192,22 +191,28 @@ def _c5_rehearsal(world, ckpt, extra=()):
     if world == 1:
         cmd = [sys.executable, tool] + args
     else:
-        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-               "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", tool] + args
-    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+        cmd = [sys.executable, "-m", "ldpc_sparc_amd.launch", "--nproc", str(world), tool] + args
+    env = {k: v for k, v in (env or os.environ).items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env["PYTHONPATH"] = env.get("PYTHONPATH", "") + os.pathsep + repo
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     return [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
 
 
 def test_c5_sweep_rehearsal_world8_kill_and_resume(tmp_path):
-    """The C5 sweep driver at 8 ranks (gloo rehearsal of the RCCL path):
-    interrupted after 2 rounds of every point, then resumed from rank 0's
-    checkpoints, it ends with the same per-point counts as one uninterrupted
-    rank; the interrupted run stopped short of them."""
-    one = _c5_rehearsal(1, str(tmp_path / "one"))
-    part = _c5_rehearsal(8, str(tmp_path / "eight"), ["--max-rounds", "2"])
-    full = _c5_rehearsal(8, str(tmp_path / "eight"))
+    """The C5 sweep driver at 8 ranks (host-rendezvous rehearsal of the RCCL
+    path), with torch not importable: interrupted after 2 rounds of every
+    point, then resumed from rank 0's checkpoints, it ends with the same
+    per-point counts as one uninterrupted rank; the interrupted run stopped
+    short of them."""
+    stub = tmp_path / "notorch" / "torch"
+    stub.mkdir(parents=True)
+    (stub / "__init__.py").write_text("raise ImportError('torch is blocked in this test')\n")
+    env = dict(os.environ, PYTHONPATH=str(tmp_path / "notorch"))
+    one = _c5_rehearsal(1, str(tmp_path / "one"), env=env)
+    part = _c5_rehearsal(8, str(tmp_path / "eight"), ["--max-rounds", "2"], env=env)
+    full = _c5_rehearsal(8, str(tmp_path / "eight"), env=env)
     keys = ("codewords", "ber", "fer", "unprotected_bit_errors", "protected_bit_errors")
     assert [[p[k] for k in keys] for p in full[:-1]] == [[p[k] for k in keys] for p in one[:-1]]
     assert full[-1]["gpus"] == 8 and full[-1]["rehearsal"]

@@ -4,13 +4,12 @@ codewords sharded over the GPUs of one node with one RCCL all-reduce of the
 error counters per round (montecarlo.concat_ber_sweep).
 
   python tools/c5_sweep.py --codewords 10000000 --ebn0 1 2 3 4 5 6
-  python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
-      tools/c5_sweep.py --codewords 10000000
+  python -m ldpc_sparc_amd.launch --nproc 8 tools/c5_sweep.py --codewords 10000000
 
 Prints one JSON line per point on rank 0; --npz writes the arrays in the
 layout of ldpc_sparc/performance_plots_general.py:138.
 
---rehearsal runs the same sharding, counter all-reduce (gloo instead of RCCL),
+--rehearsal runs the same sharding, counter all-reduce (the host rendezvous group instead of RCCL),
 checkpointing and npz output on the CPU with a synthetic trial in place of the
 GPU pipeline (deterministic counters per (seed, point, block), so the totals
 do not depend on the rank count); --max-rounds interrupts every point after
@@ -26,6 +25,7 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ldpc_sparc_amd import _native, montecarlo  # noqa: E402
+from ldpc_sparc_amd.rendezvous import HostGroup  # noqa: E402
 
 
 class SyntheticConcatTrial:
@@ -77,23 +77,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     agg = montecarlo.Aggregator()
     trial = None
-    if world > 1:
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+    group = HostGroup(rank, world) if world > 1 else None  # stdlib TCP rendezvous (no PyTorch)
     if args.rehearsal:
         from ldpc_sparc_amd.ldpc import code
         user_bits = args.L_unprotected * int(np.log2(args.M)) + args.mults * code("802.11n", "1/2", 81).K
         trial = SyntheticConcatTrial(args.ebn0, user_bits, args.seed)
         if world > 1:
-            agg = montecarlo.Aggregator("gloo")
+            agg = montecarlo.Aggregator("host", group=group)
     else:
         _native.require_gpu()
         _native.check(_native.lib().sg_set_device(local % max(_native.device_count(), 1)))
         if world > 1:
-            obj = [_native.Comm.unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(obj, src=0)
-            agg = montecarlo.Aggregator("rccl", _native.Comm(world, rank, obj[0]))
+            uid = group.bcast_bytes(_native.Comm.unique_id() if rank == 0 else b"")
+            agg = montecarlo.Aggregator("rccl", _native.Comm(world, rank, uid))
     t0 = time.perf_counter()
     res = montecarlo.concat_ber_sweep(args.L, args.M, args.n, args.P, args.L_unprotected, args.mults, args.ebn0,
                                       codewords=int(args.codewords), block=args.block,
@@ -107,9 +103,9 @@ def main():
         tot = sum(r["codewords"] for r in res)
         print(json.dumps({"codewords": tot, "seconds": el, "codewords_per_s": tot / el, "gpus": world,
                           "rehearsal": bool(args.rehearsal)}), flush=True)
-    if world > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
+    if group is not None:
+        group.barrier()
+        group.close()
 
 
 if __name__ == "__main__":
