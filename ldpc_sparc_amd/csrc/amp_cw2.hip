@@ -92,6 +92,19 @@ static_assert(C2_EPT == 16, "the transform is written for 16 values per thread")
 #define C2_AB_PF 1
 #endif
 
+// Section statistics: in cw2_az (class copy and two-pass scan per class, merged over the classes, then
+// cw2_merge: 0), or in their own full-occupancy launch after cw2_az (cw2_stats: one wavefront per section
+// reading its class segments of s from HBM, then cw2_final: 1), the f64 engine's form (amp_cw2d.hip) (A/B)
+#ifndef C2_STATS_LAUNCH
+#define C2_STATS_LAUNCH 0
+#endif
+// Az rows' per-codeword class-invariant input (a thread's scaled z / phi, 24 VGPRs at 12 slots) loaded once per
+// launch and held in registers across the class loop (1; with the statistics launch cw2_az has the registers),
+// or re-read from L2 / MALL every class (0) (A/B); the slot words are the plan's, shared by every codeword
+#ifndef C2_AZ_HOLD
+#define C2_AZ_HOLD 0
+#endif
+
 // exp(x / tau) as exp2(x * (log2 e / tau)): __expf lowers to a multiply by log2 e and v_exp_f32, so
 // with log2 e folded into the per-codeword scale every exponential is one instruction
 constexpr double C2_LOG2E = 1.4426950408889634074;
@@ -711,6 +724,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
     const float *vz = tb.vz + (size_t)cw * (cw2_vz_tm(OT) ? OTP : OT) * C2_T * (C2_POLAR ? 2 : 1);
     // running statistics of sections tid and tid + 512 over this half's classes
     const int Lb = tb.Lblk;
+#if !C2_STATS_LAUNCH
     float Mr[2] = {-INFINITY, -INFINITY}, R1[2] = {0.f, 0.f}, R2[2] = {0.f, 0.f}, st[2] = {NAN, NAN};
     int jt[2] = {-1, -1};
 #pragma unroll
@@ -718,9 +732,25 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
         const int sec = tid + k * C2_T;
         if (bf.true_idx && sec < Lb) jt[k] = tb.qpos[sec * tb.M + bf.true_idx[lb + sec]];
     }
+#else
+    (void)lb;
+    (void)Lb;
+    (void)inv_tau;
+#endif
     const int Qh = tb.Q >> 1;
     c2_tw1_init<true>(tid);
     const int *cpl = c2_stage_cp(smem, tb, tid);
+    constexpr bool HOLD = C2_AZ_HOLD && C2_POLAR && OT <= 12;
+    c2f vhold[HOLD ? OT : 1];
+    if constexpr (HOLD) {
+        const __amdgpu_buffer_rsrc_t rv = c2_rsrc(vz, 8 * OTP * C2_T);
+#pragma unroll
+        for (int q = 0; q < OTP / 2; ++q) {
+            const auto w = __builtin_amdgcn_raw_buffer_load_b128(rv, 8 * OTP * tid, 16 * q, 0);
+            if (2 * q < OT) vhold[2 * q] = c2f{__uint_as_float(w[0]), __uint_as_float(w[1])};
+            if (2 * q + 1 < OT) vhold[2 * q + 1] = c2f{__uint_as_float(w[2]), __uint_as_float(w[3])};
+        }
+    }
     __syncthreads();  // the staged statistics
     C2_TP(42);
     for (int m2 = h * Qh; m2 < (h + 1) * Qh; ++m2) {
@@ -737,22 +767,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
         constexpr bool EARLY = OT <= 12;
         float v[C2_SN];
         uint32_t e[C2_SN];
-        auto load_slice = [&]() {
-#if C2_AZPOS
-            // the entries' image positions two per word (clsp: entries i and i + 9 of the thread), half the
-            // table loads and bytes of the full words (the sections are not needed here)
-            const __amdgpu_buffer_rsrc_t re = c2_rsrc(tb.clsp + (size_t)m2 * (CW2_SLICE / 2), 2 * CW2_SLICE);
-#pragma unroll
-            for (int i = 0; i < C2_SN / 2; ++i) {
-                const uint32_t w = c2_ldu(re, 4 * tl, 4 * i * C2_T);
-                e[i] = w & 0xffffu;
-                e[i + C2_SN / 2] = w >> 16;
-            }
-#else
-            const __amdgpu_buffer_rsrc_t re = c2_rsrc(tb.cls2 + (size_t)m2 * CW2_SLICE, 4 * CW2_SLICE);
-#pragma unroll
-            for (int i = 0; i < C2_SN; ++i) e[i] = c2_ldu(re, 4 * tl, 4 * i * C2_T);
-#endif
+        auto load_v = [&]() {  // beta_prev of the class slice
 #pragma unroll
             for (int i = 0; i < C2_SN; ++i) {
                 if (C2_SKIP(128)) {  // (synthetic entries inside the image, section 0)
@@ -762,6 +777,25 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
                 }
                 v[i] = c2_ldf(rs, 4 * tl + 4 * i * C2_T, 0);  // (t = 0: unused)
             }
+        };
+        // the entries' positions and (HOLD 0) beta_prev; with the scaled z / phi held in registers (HOLD) beta_prev
+        // is requested after the transform (in flight across it beside the held values, it spills)
+        auto load_slice = [&]() {
+#if C2_AZPOS
+            // the entries' image positions two per word (clsp: entries i and i + 9 of the thread), half the
+            // table loads and bytes of the full words (the sections are not needed here)
+            const __amdgpu_buffer_rsrc_t re = c2_rsrc(tb.clsp + (size_t)m2 * (CW2_SLICE / 2), 2 * CW2_SLICE);
+#pragma unroll
+            for (int i = 0; i < C2_SN / 2; ++i) {
+                const uint32_t w = c2_ldu(re, 4 * tl, 4 * i * C2_T);
+                e[i] = w;  // (packed: entries i and i + 9, unpacked at the gather -- 9 VGPRs across the transform)
+            }
+#else
+            const __amdgpu_buffer_rsrc_t re = c2_rsrc(tb.cls2 + (size_t)m2 * CW2_SLICE, 4 * CW2_SLICE);
+#pragma unroll
+            for (int i = 0; i < C2_SN; ++i) e[i] = c2_ldu(re, 4 * tl, 4 * i * C2_T);
+#endif
+            if constexpr (!HOLD) load_v();
         };
 #if C2_POLAR
         if (!C2_SKIP(16)) {  // rows r and P - r of each owned pair: sum of al v conj(W) / be v W over its outputs
@@ -778,7 +812,11 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
                                          rk = c2_rsrc(cw2_vz_tm(OT) ? tb.kat : tb.ka, 4 * OTP * C2_T);
             uint32_t kall[CH == OT ? OT : 1];
             c2f vall[CH == OT ? OT : 1];
-            if constexpr (CH == OT) {  // one load round: a thread's slot words and scaled z / phi, 16-byte loads
+            if constexpr (HOLD) {  // the slot words (shared by every codeword: L2 hits) reloaded per class
+                if (!C2_SKIP(32)) c2_ld_slots<OT>(rk, tl, kall);
+#pragma unroll
+                for (int j = 0; j < OT; ++j) vall[j] = vhold[j];
+            } else if constexpr (CH == OT) {  // one load round: a thread's slot words and scaled z / phi, 16-byte loads
                 if (!C2_SKIP(32)) {
                     c2_ld_slots<OT>(rk, tl, kall);
 #pragma unroll
@@ -909,6 +947,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
         // (requested after the rows' table loads: vector-memory loads complete in order, so a slice
         // requested before them would hold the rows up for its whole HBM latency)
         if constexpr (EARLY) load_slice();
+#if !C2_STATS_LAUNCH
         int sa[2], sb[2];  // the sections' segments of the class (in flight during the transform; sections
                            // past Lb read 0 as their end: empty)
         {
@@ -920,6 +959,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
                 sb[k] = __builtin_amdgcn_raw_buffer_load_b16(rg, 2 * sec + 2, 0, 0);
             }
         }
+#endif
         C2_TPC(33);
         __syncthreads();
         C2_TPC(34);
@@ -929,11 +969,14 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
         C2_TPC(35);
         float snv[C2_SN];
         if constexpr (!EARLY) load_slice();
+        if constexpr (HOLD) load_v();
         {
 #pragma unroll
             for (int i = 0; i < C2_SN; ++i) {  // s = beta_prev + tau u (sparc.py:972); beta_prev stored by cw2_ab
                 const float b = have_beta ? v[i] : 0.f;
-                snv[i] = b + tau * (C2_SKIP(1024) ? (float)i : dr[C2_AZPOS ? e[i] : e[i] & 0xffffu]);
+                const uint32_t pos = C2_AZPOS ? (i < C2_SN / 2 ? e[i] & 0xffffu : e[i - C2_SN / 2] >> 16)
+                                              : e[i] & 0xffffu;
+                snv[i] = b + tau * (C2_SKIP(1024) ? (float)i : dr[pos]);
             }
         }
         C2_TPC(36);
@@ -945,6 +988,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
         C2_TPC(37);
         __syncthreads();
         C2_TPC(38);
+#if !C2_STATS_LAUNCH
         if (!C2_SKIP(64)) {
 #pragma unroll
         for (int c = 0; c < C2_SN; ++c) dr[tl + c * C2_T] = snv[c];  // s of the class in class order (past the
@@ -1040,14 +1084,138 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
         }  // (C2_SKIP(64))
         C2_TPC(40);
         __syncthreads();  // the next class overwrites the image
+#endif
         C2_TPC(41);
     }
     C2_TP(43);
+#if !C2_STATS_LAUNCH
     float4 *part = tb.part + ((size_t)cw * 2 + h) * Lb;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         const int sec = tid + k * C2_T;
         if (sec < Lb) part[sec] = make_float4(Mr[k], R1[k], R2[k], st[k]);
+    }
+#endif
+}
+
+// ---------------------------------------------------------------------------- statistics launch
+// (C2_STATS_LAUNCH) After cw2_az: one wavefront per section, lane m its class-m segment of s (class order),
+// the section's entries k = lane + 64 j read in concatenated class order (each entry's class from an owner
+// table the classes' lanes fill); the maximum, then the sums of e = exp((x - max) / tau) and e^2 over every
+// entry but one maximum (the fract form of cw2_az's scan), the section's max and 1 / sum (the next Ab's
+// softmax, sparc.py:429-432, and a hand-over's state), and 1 - sum beta^2 and the squared error per section
+// (sparc.py:973-981) for cw2_final.  Per-lane sums, then a xor tree: a fixed order.
+constexpr int C2_ST_K = 8;  // entries per lane: sections of M <= 512 entries
+__device__ __forceinline__ float c2_wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ float c2_wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+template <int ST_W>
+__global__ __launch_bounds__(64 * ST_W) void cw2_stats(Cw2Tables tb, RegBufs<float> bf) {
+    __shared__ int bas[ST_W][64];
+    __shared__ uint8_t own[ST_W][64 * C2_ST_K];  // the class of each entry of the section
+    const int wpc = tb.Lblk / ST_W;  // workgroups per codeword
+    const int w = (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int cw = blockIdx.x / wpc, l = (blockIdx.x % wpc) * ST_W + w;
+    if (!bf.active[cw]) return;
+    const size_t lb = (size_t)cw * tb.L;
+    const float inv_tau = (float)(C2_LOG2E / bf.tau[cw]);  // log2 e / tau (c2_exp2)
+    const float *s = bf.s + (size_t)cw * tb.LM;
+    int p0 = 0, n = 0;
+    if (lane < tb.Q) {
+        const uint16_t *sg = tb.seg + (size_t)lane * (tb.Lblk + 1);
+        p0 = tb.cls_ptr[lane] + sg[l];
+        n = sg[l + 1] - sg[l];
+    }
+    int inc = n;  // inclusive scan over the lanes
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
+    }
+    const int total = __shfl(inc, 63, 64);  // the section's entries (M)
+    bas[w][lane] = p0 - (inc - n);
+    for (int k = inc - n; k < inc; ++k) own[w][k] = (uint8_t)lane;
+    float st = 0.f;
+    if (bf.true_idx && lane == 0) st = s[tb.qpos[l * tb.M + bf.true_idx[lb + l]]];  // (in flight meanwhile)
+    __syncthreads();
+    float x[C2_ST_K];
+#pragma unroll
+    for (int j = 0; j < C2_ST_K; ++j) {
+        const int k = lane + 64 * j;
+        const bool in = k < total;
+        const int ad = in ? bas[w][own[w][k]] + k : 0;
+        const float v = s[ad];
+        x[j] = in ? v : -INFINITY;
+    }
+    float m = x[0];
+#pragma unroll
+    for (int j = 1; j < C2_ST_K; ++j) m = fmaxf(m, x[j]);
+    m = c2_wave_max(m);
+    float S1 = 0.f, S2 = 0.f, Se = 0.f;
+#pragma unroll
+    for (int j = 0; j < C2_ST_K; ++j) {  // (past the section: exp2(-inf) = 0)
+        const float ex = c2_exp2((x[j] - m) * inv_tau);
+        const float f = __builtin_amdgcn_fractf(ex);
+        S1 += f;
+        S2 += f * f;
+        Se += ex;
+    }
+    S1 = c2_wave_sum(S1);
+    S2 = c2_wave_sum(S2);
+    Se = c2_wave_sum(Se);
+    if (lane == 0) {
+        const float ties = rintf(Se - S1) - 1.f;  // entries equal to the maximum, but one
+        if (ties > 0.f) {
+            S1 += ties;
+            S2 += ties;
+        }
+        const float inv = 1.f / (1.f + S1);
+        bf.stM[lb + l] = m;
+        bf.stI[lb + l] = inv;
+        // 1 - sum beta^2 = (2 R1 + R1^2 - R2) / (1 + R1)^2, no cancellation (as cw2_merge)
+        const double i2 = (double)inv * (double)inv, r1 = S1, r2 = S2;
+        double er = 0.0;
+        if (bf.true_idx) {
+            if (st == m) {
+                er = (r1 * r1 + r2) * i2;
+            } else {
+                const double bt = (double)(c2_exp2((st - m) * inv_tau) * inv);
+                er = (1.0 + r2) * i2 - 2.0 * bt + 1.0;
+            }
+        }
+        reinterpret_cast<double2 *>(tb.part)[lb + l] = make_double2((2.0 * r1 + r1 * r1 - r2) * i2, er);
+    }
+}
+
+// psi, NMSE and the stopping rule from the summed sections (sparc.py:973-988); thread 0
+__device__ __forceinline__ void c2_psi_stop(const RegBufs<float> &bf, const AmpScalars &sc, const AmpParams &pr, int cw, int t,
+                                            double denom, double a, double er) {
+    if (threadIdx.x == 0) {
+        double *psi = sc.psi + cw, *psi_prev = sc.psi_prev + cw;
+        double *nmse = sc.nmse + (size_t)cw * pr.t_max;
+        const double pnew = a / denom;
+        *psi = pnew;
+        nmse[t + 1] = er / denom;
+        bool stop = false;
+        if (t > 0 && C2_ABL == 0) {  // (ablation builds never stop early: every launch does the same work)
+            const double pp = *psi_prev;
+            stop = fabs(pnew - pp) <= pr.atol + pr.rtol * fabs(pp);  // sparc.py:984-986
+        }
+        if (stop) {  // nmse[t:] = nmse[t] (sparc.py:985)
+            for (int tt = t + 1; tt < pr.t_max; ++tt) nmse[tt] = nmse[t];
+            sc.t_final[cw] = t + 1;
+            bf.active[cw] = 0;
+        } else if (t == pr.t_max - 2) {
+            sc.t_final[cw] = t + 1;
+            bf.active[cw] = 0;
+        }
     }
 }
 
@@ -1099,27 +1267,24 @@ __global__ __launch_bounds__(1024) void cw2_merge(Cw2Tables tb, RegBufs<float> b
         }
     }
     c2_block_sum2(a, er, red);
-    if (tid == 0) {
-        double *psi = sc.psi + cw, *psi_prev = sc.psi_prev + cw;
-        double *nmse = sc.nmse + (size_t)cw * pr.t_max;
-        const double denom = (double)tb.L;
-        const double pnew = a / denom;
-        *psi = pnew;
-        nmse[t + 1] = er / denom;
-        bool stop = false;
-        if (t > 0 && C2_ABL == 0) {  // (ablation builds never stop early: every launch does the same work)
-            const double pp = *psi_prev;
-            stop = fabs(pnew - pp) <= pr.atol + pr.rtol * fabs(pp);  // sparc.py:984-986
-        }
-        if (stop) {  // nmse[t:] = nmse[t] (sparc.py:985)
-            for (int tt = t + 1; tt < pr.t_max; ++tt) nmse[tt] = nmse[t];
-            sc.t_final[cw] = t + 1;
-            bf.active[cw] = 0;
-        } else if (t == pr.t_max - 2) {
-            sc.t_final[cw] = t + 1;
-            bf.active[cw] = 0;
-        }
+    c2_psi_stop(bf, sc, pr, cw, t, (double)tb.L, a, er);
+}
+
+// (C2_STATS_LAUNCH) the sections' sums of cw2_stats -> psi, NMSE, stop, in cw2_merge's summation order
+__global__ __launch_bounds__(1024) void cw2_final(Cw2Tables tb, RegBufs<float> bf, AmpScalars sc, AmpParams pr,
+                                                  int t) {
+    __shared__ double red[32];
+    const int cw = blockIdx.x, tid = threadIdx.x;
+    if (!bf.active[cw]) return;
+    const size_t lb = (size_t)cw * tb.L;
+    double a = 0.0, er = 0.0;
+    if (tid < tb.Lblk) {  // (one section per thread, the merge's summation order)
+        const double2 v = reinterpret_cast<const double2 *>(tb.part)[lb + tid];
+        a = v.x;
+        er = v.y;
     }
+    c2_block_sum2(a, er, red);
+    c2_psi_stop(bf, sc, pr, cw, t, (double)tb.L, a, er);
 }
 
 // z of every codeword in natural order from its slot-order copy (cw2_ctrl keeps z in slot order only): run
@@ -1170,7 +1335,15 @@ static int cw2_launch(const Cw2Tables &tb, const RegBufs<float> &bf, const AmpSc
     }
     {
         ProfScope ps(SG_PH_CW2_CTRL, s);
-        hipLaunchKernelGGL((cw2_merge), gB, dim3(1024), 0, s, tb, bf, sc, pr, t);
+        if (C2_STATS_LAUNCH) {
+            if (tb.Lblk % 16 == 0)
+                hipLaunchKernelGGL((cw2_stats<16>), dim3(bf.B * (tb.Lblk / 16)), dim3(64 * 16), 0, s, tb, bf);
+            else
+                hipLaunchKernelGGL((cw2_stats<4>), dim3(bf.B * (tb.Lblk / 4)), dim3(64 * 4), 0, s, tb, bf);
+            hipLaunchKernelGGL((cw2_final), gB, dim3(1024), 0, s, tb, bf, sc, pr, t);
+        } else {
+            hipLaunchKernelGGL((cw2_merge), gB, dim3(1024), 0, s, tb, bf, sc, pr, t);
+        }
     }
     return SG_OK;
 }
@@ -1179,7 +1352,8 @@ int cw2_launch_iter(const Cw2Tables &tb, const RegBufs<float> &bf, const AmpScal
                     hipStream_t s) {
     if (bf.B <= 0) return SG_OK;
     if (tb.Q % 2 || tb.L > 1024 || tb.Lblk > 2 * C2_T || tb.maxcls > C2_NC * C2_SC * C2_T ||
-        fpad(tb.maxcls + 16) >= 2 * C2_P || tb.N2 != C2_P * tb.Q)
+        fpad(tb.maxcls + 16) >= 2 * C2_P || tb.N2 != C2_P * tb.Q ||
+        (C2_STATS_LAUNCH && (tb.Lblk != tb.L || tb.L % 4 || tb.M > 64 * C2_ST_K || tb.Q > 64)))
         return fail(SG_ERR_UNSUPPORTED, "split per-codeword engine: sizes outside its compile-time bounds");
     ProfScope ps(SG_PH_AMP_CW, s);
     switch (tb.OT) {

@@ -34,6 +34,8 @@ fetch, nd = load(sys.argv[1], "FETCH_SIZE")
 write, _ = load(sys.argv[2], "WRITE_SIZE")
 lines = [l for l in open(sys.argv[3]).read().splitlines() if l.startswith("{")]
 bench = json.loads(lines[-1])
+if bench.get("detail") and os.path.exists(bench["detail"]):  # the compact line names the full record
+    bench = json.load(open(bench["detail"]))
 per = {}
 for k in sorted(set(fetch) | set(write)):
     d = max(nd.get(k, 1), 1)

@@ -34,7 +34,8 @@ a2, _ = load(sys.argv[2])
 bench_json = sys.argv[4] if len(sys.argv) > 4 and sys.argv[4].endswith(".json") else None
 out = {}
 for k in sorted(a1):
-    prefixes = sys.argv[5 if bench_json else 4:] or ["cw_iter", "cw2_", "bp_flood_kernel", "bp_grouped"]
+    prefixes = sys.argv[5 if bench_json else 4:] or ["cw_iter", "cw2_", "cw2d_", "bp_flood_kernel", "bp_grouped",
+                                                      "blk", "gemm_", "dense_", "control_kernel"]
     if not any(k.startswith(pf) for pf in prefixes):
         continue
     c = dict(a1[k])
@@ -52,13 +53,13 @@ for k in sorted(a1):
               "valu_insts_per_wave": c.get("SQ_INSTS_VALU", 0) / max(c.get("SQ_WAVES", 1), 1)}
 LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ldpc_sparc_amd", "_lib",
                    "libldpc_sparc_amd.so")
-res = {"kernels": out, "lib_sha256": hashlib.sha256(open(LIB, "rb").read()).hexdigest()[:16], "method": "rocprofv3 --pmc, two passes of 8 SQ counters over "
-                                  "bench.py --cpu-seconds 0 --no-concat --no-r13 --no-sc --steps 2 --warmup 1 "
-                                  "--bp-steps 3; fractions of SQ_WAVE_CYCLES (summed over waves)"}
+res = {"kernels": out, "lib_sha256": hashlib.sha256(open(LIB, "rb").read()).hexdigest()[:16],
+       "method": "rocprofv3 --pmc, two passes of 8 SQ counters over a short bench.py run (tools/pmc_sq_bench.sh: "
+                 + os.environ.get("SQ_ARGS_USED", "") + "); fractions of SQ_WAVE_CYCLES (summed over waves)"}
 if bench_json:
     lines = [l for l in open(bench_json).read().splitlines() if l.startswith("{")]
     rf = json.loads(lines[-1]).get("roofline", {}) if lines else {}
-    c2k = [k for k in out if k.startswith("cw2_")]
+    c2k = [k for k in out if k.startswith("cw2_") and not k.startswith("cw2d_")]
     naz = sum(out[k]["dispatches"] for k in c2k if k.startswith("cw2_az"))
     if c2k and naz and rf.get("codeword_iterations_per_launch"):
         cwit = rf["codeword_iterations_per_launch"] * naz

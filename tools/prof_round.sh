@@ -10,7 +10,7 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/prof; rm -rf $O; mkdir -p $O
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/ks -o run --output-format csv -- python bench.py --cpu-seconds 0 --bp-ebn0-extra --steps 10 --warmup 2 > $O/bench.json 2> $O/bench.err
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/ks -o run --output-format csv -- python bench.py --cpu-seconds 0 --bp-ebn0-extra --steps 10 --warmup 2 --detail-dir $O > $O/bench.json 2> $O/bench.err
 bash tools/pmc_bench.sh
 bash tools/pmc_sq_bench.sh
 bash tools/pmc_concat.sh
