@@ -662,8 +662,10 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
         return best <= 1e-12 * (std::abs(o.al) + std::abs(o.be) + 1e-300);
     };
     if (p->precision != SG_F64 && !pow2) return SG_OK;
+    std::vector<uint32_t> last_word(T, 0u);
     for (int tid = 0; tid < T; ++tid) {
         int j = 0;
+        if (own[tid].empty()) return SG_OK;  // (amp_cw2.hip's rows write where the thread's last pair is)
         for (int r : own[tid]) {
             const auto &lst = pair_of[r];
             for (size_t q = 0; q < lst.size(); ++q, ++j) {
@@ -690,6 +692,7 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
                     wab[2 * c + 1] = (e & CW_SELF) ? 4u * CW2_TRASH : 8u * (uint32_t)c2pos(P - r);
                 }
                 oi[c] = i;
+                last_word[tid] = e & ~(CW_VALID | CW_NEWROW);  // (the padding slots below)
                 const float v[8] = {(float)o.c1.real(), (float)o.c1.imag(), (float)o.c2.real(), (float)o.c2.imag(),
                                     (float)o.al.real(), (float)o.al.imag(), (float)o.be.real(), (float)o.be.imag()};
                 std::copy(v, v + 4, cf.begin() + 4 * c);
@@ -706,6 +709,26 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
             }
         }
     }
+    // Padding slots (after a thread's pairs; zero coefficients, zero z/phi scale, not VALID) carry the word of
+    // the thread's last output without CW_NEWROW: the f32 rows (amp_cw2.hip, C2_ROWS_ALWAYS) write every
+    // slot's running sum at its pair's rows, so a padding slot adds 0 to the last pair's sums and writes them
+    // again -- never a row of another thread's pair
+    if (p->precision != SG_F64)
+        for (int tid = 0; tid < T; ++tid)
+            for (int j = 0; j < OT; ++j) {
+                uint32_t &e = ka[(size_t)j * T + tid];
+                if (!(e & CW_VALID)) e = last_word[tid];
+            }
+    // Padding slots (after a thread's pairs; zero coefficients, zero z/phi scale, not VALID) carry the word of
+    // the thread's last output without CW_NEWROW: the f32 rows (amp_cw2.hip, C2_ROWS_ALWAYS) write every
+    // slot's running sum at its pair's rows, so a padding slot adds 0 to the last pair's sums and writes them
+    // again -- never a row of another thread's pair
+    if (p->precision != SG_F64)
+        for (int tid = 0; tid < T; ++tid)
+            for (int j = 0; j < OT; ++j) {
+                uint32_t &e = ka[(size_t)j * T + tid];
+                if (!(e & CW_VALID)) e = last_word[tid];
+            }
     // Which image values the class scatter (Ab, class m2 < Q) and the row
     // writes (Az, entry Q) leave behind, as bits of the thread that reads
     // them in the first FFT stage (c2_stage0_r32: complex index m1 = j + 256 g
