@@ -179,10 +179,193 @@ __global__ __launch_bounds__(256, MT == 4 ? 2 : 1) void gemm_f32_mfma(GemmF32 g)
         }
 }
 
+// ------------------------------------------------------------------ f32 MFMA GEMM, LDS-DMA staging
+// The same product and block tile with the operand tiles moved global -> LDS by global_load_lds_dwordx4
+// (no staging registers, no LDS store instructions), K tiles of 16 in two LDS buffers: the DMA of tile t + 1
+// is in flight while the MFMAs run on tile t, one barrier per tile.  A DMA writes 1 KiB per wave-instruction
+// lane-linearly, so the conflict-free read layout comes from the source addresses: a 16-float row of the X
+// (and NT Y) tile holds its four 16-byte groups at slot g ^ ((row >> 2) & 3), and each lane reads its 8
+// k-values (k = 8 h + kk, h = lane >> 5, kk = 0..7: the MFMA's k pair at step kk is {kk, 8 + kk}) as two
+// ds_read_b128 -- 16 consecutive rows of one read cover all 16 slots of a bank row.  The NN Y tile ([k][n],
+// 512-byte rows) is read along n as before.  Every output's k order is the same for both MT, so the two
+// block heights still agree bit for bit (a different order from gemm_f32_mfma's, so not with it).
+// Needs tiles without ragged K (the K chunk a multiple of 16) and, for NN, N a multiple of 128; rows past M
+// or past yrows read a clamped row (their products land in unstored outputs, or meet z's zero padding).
+constexpr int GBK2 = 16;
+template <int MT>
+constexpr int glds_buf_floats() { return 64 * MT * GBK2 + GBN * GBK2; }  // one buffer: the X and Y tiles
+typedef __attribute__((address_space(3))) void lds_void;
+template <bool NT, int MT>
+__global__ __launch_bounds__(256, MT == 4 ? 2 : 1) void gemm_f32_glds(GemmF32 g) {
+    constexpr int BM = gbm<MT>(), BUF = glds_buf_floats<MT>();
+    __shared__ __attribute__((aligned(16))) float lds[2 * BUF];  // two buffers, one LDS object
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid >> 1, wn = wid & 1;
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * GBN;
+    const int kb = blockIdx.z * g.kchunk;
+    const int ke = min(g.K, kb + g.kchunk);
+    const int nk = (ke - kb) / GBK2;
+    // DMA sources through buffer resources based at the block's first row (32-bit per-lane offsets; rows
+    // past M / yrows are past the resource's end and read as 0)
+    // (every resource field through readfirstlane: a resource the compiler cannot prove uniform gets a waterfall
+    // loop around each DMA)
+    const int ldx = __builtin_amdgcn_readfirstlane((int)g.ldx), ldy = __builtin_amdgcn_readfirstlane((int)g.ldy);
+    const int nrx = __builtin_amdgcn_readfirstlane(4 * ldx * max(0, min(BM, g.M - m0)));
+    const int nry = __builtin_amdgcn_readfirstlane(4 * ldy * max(0, min(GBN, g.yrows - n0)));
+    const __amdgpu_buffer_rsrc_t rx =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(g.X + (long)m0 * ldx), 0, nrx, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ry =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(g.Y + (long)n0 * ldy), 0, nry, 0x00020000);
+    // per-lane source offsets (tile-invariant) and the wave's LDS destinations
+    int ox[BM / 64], oy[2];
+#pragma unroll
+    for (int i = 0; i < BM / 64; ++i) {
+        const int row = 16 * (i * 4 + wid) + (lane >> 2);
+        ox[i] = 4 * row * ldx + 16 * ((lane & 3) ^ ((row >> 2) & 3));
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        if (NT) {
+            const int row = 16 * (i * 4 + wid) + (lane >> 2);
+            oy[i] = 4 * row * ldy + 16 * ((lane & 3) ^ ((row >> 2) & 3));
+        } else {
+            oy[i] = 4 * (2 * (i * 4 + wid) + (lane >> 5)) * ldy + 16 * (lane & 31);
+        }
+    }
+    auto stage = [&](int buf, int k0) {
+        float *bx = lds + buf * BUF, *by = bx + BM * GBK2;
+        // X: BM rows x 4 slots = BM / 16 wave-instructions of 16 rows
+#pragma unroll
+        for (int i = 0; i < BM / 64; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_void *)(bx + 256 * (i * 4 + wid)), 16, ox[i], 4 * k0, 0, 0);
+        if (NT) {  // 128 n-rows x 4 slots
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(ry, (lds_void *)(by + 256 * (i * 4 + wid)), 16, oy[i], 4 * k0, 0,
+                                                         0);
+        } else {  // 16 k-rows x 128 n, two k-rows per wave-instruction (A is 19 GB at C5: a resource per tile)
+            const int nrk = __builtin_amdgcn_readfirstlane(4 * ldy * max(0, min(GBK2, g.yrows - k0)));
+            const __amdgpu_buffer_rsrc_t rk =
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(g.Y + (long)k0 * ldy + n0), 0, nrk, 0x00020000);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (lds_void *)(by + 256 * (i * 4 + wid)), 16, oy[i], 0, 0, 0);
+        }
+    };
+    f32x16 acc[MT][2];
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+    const int h = lane >> 5, rl = lane & 31;
+    if (nk > 0) stage(0, kb);
+    for (int kt = 0; kt < nk; ++kt) {
+        // tile kt landed (the barrier's fence waits for this wave's DMAs), and every wave has read its fragments
+        // of tile kt - 1, so the other buffer is free
+        if (GEMM_PRIO) __builtin_amdgcn_s_setprio(0);
+        __syncthreads();
+        // the whole tile's fragments first (k = 8 h + 4 q + 0..3), THEN the next tile's DMA: with a DMA in flight
+        // the compiler waits vmcnt(0) before any LDS read of the same object
+        const float *bx = lds + (kt & 1) * BUF, *by = bx + BM * GBK2;
+        float4 av[MT][2], bv[2][2];
+        float bn[2][GBK2 / 2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+                const int row = wm * 32 * MT + mt * 32 + rl;
+                av[mt][q] = *reinterpret_cast<const float4 *>(bx + 16 * row + 4 * ((2 * h + q) ^ ((row >> 2) & 3)));
+            }
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+                if (NT) {
+                    const int row = wn * 64 + nt * 32 + rl;
+                    bv[nt][q] = *reinterpret_cast<const float4 *>(by + 16 * row + 4 * ((2 * h + q) ^ ((row >> 2) & 3)));
+                } else {
+#pragma unroll
+                    for (int k4 = 0; k4 < 4; ++k4)
+                        bn[nt][4 * q + k4] = by[(8 * h + 4 * q + k4) * GBN + wn * 64 + nt * 32 + rl];
+                }
+            }
+        }
+        if (kt + 1 < nk) stage((kt + 1) & 1, kb + (kt + 1) * GBK2);
+        if (GEMM_PRIO) __builtin_amdgcn_s_setprio(GEMM_PRIO);
+#pragma unroll
+        for (int kk = 0; kk < GBK2 / 2; ++kk) {
+            const int q = kk >> 2, k4 = kk & 3;
+            float a[MT], b[2];
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+                const float4 v = av[mt][q];
+                a[mt] = k4 == 0 ? v.x : k4 == 1 ? v.y : k4 == 2 ? v.z : v.w;
+            }
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+                if (NT) {
+                    const float4 v = bv[nt][q];
+                    b[nt] = k4 == 0 ? v.x : k4 == 1 ? v.y : k4 == 2 ? v.z : v.w;
+                } else {
+                    b[nt] = bn[nt][kk];
+                }
+            }
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt)
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
+        }
+    }
+    float *C = g.C + (long)blockIdx.z * g.c_split;
+    const int rmax = g.M - 1, cmax = g.N - 1;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+            float av2[16];
+            if (g.add) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = m0 + wm * 32 * MT + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    const int col = n0 + wn * 64 + nt * 32 + (lane & 31);
+                    av2[r] = g.add[(long)min(row, rmax) * g.ldc + min(col, cmax)];
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + wm * 32 * MT + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                const int col = n0 + wn * 64 + nt * 32 + (lane & 31);
+                if (row < g.M && col < g.N) {
+                    const long o = (long)row * g.ldc + col;
+                    C[o] = g.add ? av2[r] + acc[mt][nt][r] : acc[mt][nt][r];
+                }
+            }
+        }
+}
+
+// the LDS-DMA kernel (1) or the register-staged one (0) (A/B); the DMA kernel only where its tiles are whole
+#ifndef GEMM_GLDS
+#define GEMM_GLDS 0
+#endif
+static bool glds_ok(const GemmF32 &g, bool nt) {
+    // whole K tiles, 16-byte aligned rows, whole NN column tiles, 32-bit per-block offsets
+    return GEMM_GLDS && g.K % GBK2 == 0 && g.kchunk % GBK2 == 0 && g.ldx % 4 == 0 && g.ldy % 4 == 0 &&
+           (nt || g.N % GBN == 0) && g.M > 0 && g.yrows > 0 && 4.0 * g.ldx * gbm<4>() < 2147483647.0 &&
+           4.0 * g.ldy * GBN < 2147483647.0;
+}
+
 // Block rows of 256 once the batch exceeds 128 codewords (A read ceil(B / 256)
 // times instead of ceil(B / 128)); 128 below that (no idle half tile).
 template <bool NT>
 static void gemm_launch(const GemmF32 &g, unsigned gx, unsigned gz, hipStream_t s) {
+    if (glds_ok(g, NT)) {
+        if (g.M > gbm<2>())
+            hipLaunchKernelGGL((gemm_f32_glds<NT, 4>), dim3(gx, (g.M + gbm<4>() - 1) / gbm<4>(), gz), dim3(256), 0, s, g);
+        else
+            hipLaunchKernelGGL((gemm_f32_glds<NT, 2>), dim3(gx, (g.M + gbm<2>() - 1) / gbm<2>(), gz), dim3(256), 0, s, g);
+        return;
+    }
     if (g.M > gbm<2>())
         hipLaunchKernelGGL((gemm_f32_mfma<NT, 4>), dim3(gx, (g.M + gbm<4>() - 1) / gbm<4>(), gz), dim3(256), 0, s, g);
     else
