@@ -192,9 +192,21 @@ __global__ __launch_bounds__(256, MT == 4 ? 2 : 1) void gemm_f32_mfma(GemmF32 g)
 // Needs tiles without ragged K (the K chunk a multiple of 16) and, for NN, N a multiple of 128; rows past M
 // or past yrows read a clamped row (their products land in unstored outputs, or meet z's zero padding).
 constexpr int GBK2 = 16;
+// the LDS-DMA kernel where its tiles are whole (1), or the register-staged kernel everywhere (0) (A/B): C5 GEMM
+// 0.864 -> 0.868 / 0.871 of the f32 MFMA peak same box, the C5 and dense tests green
+// (profiles/r06_gemm_glds_ab.txt)
+#ifndef GEMM_GLDS
+#define GEMM_GLDS 1
+#endif
 template <int MT>
 constexpr int glds_buf_floats() { return 64 * MT * GBK2 + GBN * GBK2; }  // one buffer: the X and Y tiles
 typedef __attribute__((address_space(3))) void lds_void;
+// one 16-byte-per-lane DMA global -> LDS (buffer_load_dwordx4 ... lds): lane i's 16 bytes land at lds + 16 i
+// (a non-template device function: the builtin inside the kernel template kept the host pass from emitting its
+// launch stubs)
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, float *lds, int vo, int so) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void *)lds, 16, vo, so, 0, 0);
+}
 template <bool NT, int MT>
 __global__ __launch_bounds__(256, MT == 4 ? 2 : 1) void gemm_f32_glds(GemmF32 g) {
     constexpr int BM = gbm<MT>(), BUF = glds_buf_floats<MT>();
@@ -237,19 +249,18 @@ __global__ __launch_bounds__(256, MT == 4 ? 2 : 1) void gemm_f32_glds(GemmF32 g)
         // X: BM rows x 4 slots = BM / 16 wave-instructions of 16 rows
 #pragma unroll
         for (int i = 0; i < BM / 64; ++i)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_void *)(bx + 256 * (i * 4 + wid)), 16, ox[i], 4 * k0, 0, 0);
+            dma16(rx, bx + 256 * (i * 4 + wid), ox[i], 4 * k0);
         if (NT) {  // 128 n-rows x 4 slots
 #pragma unroll
             for (int i = 0; i < 2; ++i)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(ry, (lds_void *)(by + 256 * (i * 4 + wid)), 16, oy[i], 4 * k0, 0,
-                                                         0);
+                dma16(ry, by + 256 * (i * 4 + wid), oy[i], 4 * k0);
         } else {  // 16 k-rows x 128 n, two k-rows per wave-instruction (A is 19 GB at C5: a resource per tile)
             const int nrk = __builtin_amdgcn_readfirstlane(4 * ldy * max(0, min(GBK2, g.yrows - k0)));
             const __amdgpu_buffer_rsrc_t rk =
                 __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(g.Y + (long)k0 * ldy + n0), 0, nrk, 0x00020000);
 #pragma unroll
             for (int i = 0; i < 2; ++i)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (lds_void *)(by + 256 * (i * 4 + wid)), 16, oy[i], 0, 0, 0);
+                dma16(rk, by + 256 * (i * 4 + wid), oy[i], 0);
         }
     };
     f32x16 acc[MT][2];
@@ -260,54 +271,49 @@ __global__ __launch_bounds__(256, MT == 4 ? 2 : 1) void gemm_f32_glds(GemmF32 g)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
     const int h = lane >> 5, rl = lane & 31;
-    if (nk > 0) stage(0, kb);
-    for (int kt = 0; kt < nk; ++kt) {
-        // tile kt landed (the barrier's fence waits for this wave's DMAs), and every wave has read its fragments
-        // of tile kt - 1, so the other buffer is free
-        if (GEMM_PRIO) __builtin_amdgcn_s_setprio(0);
-        __syncthreads();
-        // the whole tile's fragments first (k = 8 h + 4 q + 0..3), THEN the next tile's DMA: with a DMA in flight
-        // the compiler waits vmcnt(0) before any LDS read of the same object
-        const float *bx = lds + (kt & 1) * BUF, *by = bx + BM * GBK2;
-        float4 av[MT][2], bv[2][2];
+    // a tile's fragments in registers (k = 8 h + 4 q + 0..3)
+    struct Frag {
+        float4 a[MT][2], b[2][2];
         float bn[2][GBK2 / 2];
+    };
+    auto read_frag = [&](const float *bx, Frag &f) {
+        const float *by = bx + BM * GBK2;
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) {
                 const int row = wm * 32 * MT + mt * 32 + rl;
-                av[mt][q] = *reinterpret_cast<const float4 *>(bx + 16 * row + 4 * ((2 * h + q) ^ ((row >> 2) & 3)));
+                f.a[mt][q] = *reinterpret_cast<const float4 *>(bx + 16 * row + 4 * ((2 * h + q) ^ ((row >> 2) & 3)));
             }
 #pragma unroll
             for (int nt = 0; nt < 2; ++nt) {
                 if (NT) {
                     const int row = wn * 64 + nt * 32 + rl;
-                    bv[nt][q] = *reinterpret_cast<const float4 *>(by + 16 * row + 4 * ((2 * h + q) ^ ((row >> 2) & 3)));
+                    f.b[nt][q] = *reinterpret_cast<const float4 *>(by + 16 * row + 4 * ((2 * h + q) ^ ((row >> 2) & 3)));
                 } else {
 #pragma unroll
                     for (int k4 = 0; k4 < 4; ++k4)
-                        bn[nt][4 * q + k4] = by[(8 * h + 4 * q + k4) * GBN + wn * 64 + nt * 32 + rl];
+                        f.bn[nt][4 * q + k4] = by[(8 * h + 4 * q + k4) * GBN + wn * 64 + nt * 32 + rl];
                 }
             }
         }
-        if (kt + 1 < nk) stage((kt + 1) & 1, kb + (kt + 1) * GBK2);
-        if (GEMM_PRIO) __builtin_amdgcn_s_setprio(GEMM_PRIO);
+    };
+    auto mma = [&](const Frag &f, int q) {  // the MFMAs of k4 = 0..3 of half q of the tile
 #pragma unroll
-        for (int kk = 0; kk < GBK2 / 2; ++kk) {
-            const int q = kk >> 2, k4 = kk & 3;
+        for (int k4 = 0; k4 < 4; ++k4) {
             float a[MT], b[2];
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) {
-                const float4 v = av[mt][q];
+                const float4 v = f.a[mt][q];
                 a[mt] = k4 == 0 ? v.x : k4 == 1 ? v.y : k4 == 2 ? v.z : v.w;
             }
 #pragma unroll
             for (int nt = 0; nt < 2; ++nt) {
                 if (NT) {
-                    const float4 v = bv[nt][q];
+                    const float4 v = f.b[nt][q];
                     b[nt] = k4 == 0 ? v.x : k4 == 1 ? v.y : k4 == 2 ? v.z : v.w;
                 } else {
-                    b[nt] = bn[nt][kk];
+                    b[nt] = f.bn[nt][4 * q + k4];
                 }
             }
 #pragma unroll
@@ -316,6 +322,21 @@ __global__ __launch_bounds__(256, MT == 4 ? 2 : 1) void gemm_f32_glds(GemmF32 g)
                 for (int nt = 0; nt < 2; ++nt)
                     acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
         }
+    };
+    if (nk > 0) stage(0, kb);
+    for (int kt = 0; kt < nk; ++kt) {
+        // tile kt landed (the barrier's fence waits for this wave's DMAs), and every wave has read its fragments
+        // of tile kt - 1, so the other buffer is free
+        if (GEMM_PRIO) __builtin_amdgcn_s_setprio(0);
+        __syncthreads();
+        // the whole tile's fragments first, THEN the next tile's DMA: with a DMA in flight the compiler waits
+        // vmcnt(0) before any LDS read of the same object
+        Frag f;
+        read_frag(lds + (kt & 1) * BUF, f);
+        if (kt + 1 < nk) stage((kt + 1) & 1, kb + (kt + 1) * GBK2);
+        if (GEMM_PRIO) __builtin_amdgcn_s_setprio(GEMM_PRIO);
+        mma(f, 0);
+        mma(f, 1);
     }
     float *C = g.C + (long)blockIdx.z * g.c_split;
     const int rmax = g.M - 1, cmax = g.N - 1;
@@ -345,9 +366,6 @@ __global__ __launch_bounds__(256, MT == 4 ? 2 : 1) void gemm_f32_glds(GemmF32 g)
 }
 
 // the LDS-DMA kernel (1) or the register-staged one (0) (A/B); the DMA kernel only where its tiles are whole
-#ifndef GEMM_GLDS
-#define GEMM_GLDS 0
-#endif
 static bool glds_ok(const GemmF32 &g, bool nt) {
     // whole K tiles, 16-byte aligned rows, whole NN column tiles, 32-bit per-block offsets
     return GEMM_GLDS && g.K % GBK2 == 0 && g.kchunk % GBK2 == 0 && g.ldx % 4 == 0 && g.ldy % 4 == 0 &&
