@@ -227,6 +227,7 @@ struct Cw2Tables {
     const float4 *cf;         // [OT][512] (c1, c2): output = Re(c1 H[a] + c2 conj H[N2 - a])
     const float4 *gf;         // [OT][512] (al, be): G[a] += al z/phi, G[N2 - a] += be z/phi
     const float2 *gm;         // [OT][512] (|al|, |be|) of the polar form (CW_OFFSHIFT; cw2_ctrl scales z/phi)
+    const float4 *gmt;        // [512][OTP / 2] the same thread-major, two slots per 16 bytes (C2_VZ_HALF rows)
     int sh_off;               // log2(N / 2): the slot's phase offset o N/2 = o << sh_off
     uint32_t m4n;             // 4N - 1 (phases in units of 1 / 4N revolutions, N = 2 N2 a power of two)
     float inv_4n;             // 1 / 4N

@@ -101,14 +101,22 @@ static_assert(C2_EPT == 16, "the transform is written for 16 values per thread")
 // Az rows: every slot writes its pair's running sums at the pair's rows, addresses and factors from the slot
 // word without compares (1), or the last slot of a pair writes them, other slots write the trash slot (0) (A/B)
 #ifndef C2_ROWS_ALWAYS
-#define C2_ROWS_ALWAYS 0
+#define C2_ROWS_ALWAYS 1
+#endif
+// Polar rows' per-codeword input: z / phi alone, 4 bytes per slot, scaled in cw2_az by (|al|, |be|) from the
+// plan's thread-major table (shared by every codeword: L2-resident) (1), or the scaled pair stored by cw2_ctrl,
+// 8 bytes per slot re-read from the MALL in every class (0) (A/B; at most 12 slots per thread).  With the two
+// switches below, same box: fabric bytes 11.35 -> 9.69 MB per codeword-iteration (cw2_az 6.97 -> 5.34), C2
+// +0.4 % (profiles/r06_c2_vz_half_ab.txt)
+#ifndef C2_VZ_HALF
+#define C2_VZ_HALF 1
 #endif
 // Az statistics: the segment mask from a per-section bit mask, v_bfe + v_bfi per entry (1), or the sign-mask form
 // (0), which the compiler turns into v_cmp + v_cndmask through an SGPR pair with a hazard s_nop per entry (A/B);
 // bit-identical results.  (Pairing (x - max) / tau into v_pk_add / v_pk_mul halves their count but not their
 // issue cycles: a packed f32 instruction issues in 4 cycles, a plain one in 2 -- MI355X_MICROARCH.md.)
 #ifndef C2_ST_BITS
-#define C2_ST_BITS 0
+#define C2_ST_BITS 1
 #endif
 // Az rows' per-codeword class-invariant input (a thread's scaled z / phi, 24 VGPRs at 12 slots) loaded once per
 // launch and held in registers across the class loop (1; with the statistics launch cw2_az has the registers),
@@ -677,7 +685,16 @@ __global__ __launch_bounds__(C2_T) void cw2_ctrl(Cw2Tables tb, RegBufs<float> bf
     constexpr int OTP = cw2_otp(OT);
 #if C2_POLAR
     // z / phi times the slot's (|al|, |be|) (build_cw2 polar form), two floats per slot; padding slots 0
-    if constexpr (cw2_vz_tm(OT)) {
+    if constexpr (cw2_vz_tm(OT) && C2_VZ_HALF) {  // z / phi alone (cw2_az scales it)
+        float4 *vz4 = reinterpret_cast<float4 *>(tb.vz + ((size_t)cw * C2_T + tid) * OTP);  // thread-major
+#pragma unroll
+        for (int q = 0; q < OTP / 4; ++q) {
+            float w[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) w[c] = 4 * q + c < OT ? zr[4 * q + c] * iph : 0.f;
+            vz4[q] = make_float4(w[0], w[1], w[2], w[3]);
+        }
+    } else if constexpr (cw2_vz_tm(OT)) {
         float4 *vz4 = reinterpret_cast<float4 *>(tb.vz + ((size_t)cw * C2_T + tid) * OTP * 2);  // thread-major
 #pragma unroll
         for (int q = 0; q < OTP / 2; ++q) {
@@ -733,7 +750,8 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
     float *s = bf.s + (size_t)cw * tb.LM;
     constexpr int OTP = cw2_otp(OT);
     // [512][OTP][2] / [OT][512][2] (polar form: (|al|, |be|) z / phi); [512][OTP] / [OT][512] (C2_POLAR 0)
-    const float *vz = tb.vz + (size_t)cw * (cw2_vz_tm(OT) ? OTP : OT) * C2_T * (C2_POLAR ? 2 : 1);
+    constexpr bool VZH = C2_VZ_HALF && C2_POLAR && cw2_vz_tm(OT);
+    const float *vz = tb.vz + (size_t)cw * (cw2_vz_tm(OT) ? OTP : OT) * C2_T * (C2_POLAR && !VZH ? 2 : 1);
     // running statistics of sections tid and tid + 512 over this half's classes
     const int Lb = tb.Lblk;
 #if !C2_STATS_LAUNCH
@@ -828,6 +846,27 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
                 if (!C2_SKIP(32)) c2_ld_slots<OT>(rk, tl, kall);
 #pragma unroll
                 for (int j = 0; j < OT; ++j) vall[j] = vhold[j];
+            } else if constexpr (VZH) {  // slot words, z / phi (4 B per slot) and the plan's (|al|, |be|)
+                if (!C2_SKIP(32)) {
+                    c2_ld_slots<OT>(rk, tl, kall);
+                    const __amdgpu_buffer_rsrc_t rv1 = c2_rsrc(vz, 4 * OTP * C2_T),
+                                                 rg = c2_rsrc(tb.gmt, 8 * OTP * C2_T);
+                    float v1[OTP];
+#pragma unroll
+                    for (int q = 0; q < OTP / 4; ++q) {
+                        const auto w = __builtin_amdgcn_raw_buffer_load_b128(rv1, 4 * OTP * tl, 16 * q, 0);
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) v1[4 * q + c] = __uint_as_float(w[c]);
+                    }
+#pragma unroll
+                    for (int q = 0; q < OTP / 2; ++q) {
+                        const auto w = __builtin_amdgcn_raw_buffer_load_b128(rg, 8 * OTP * tl, 16 * q, 0);
+                        if (2 * q < OT)
+                            vall[2 * q] = c2f{__uint_as_float(w[0]), __uint_as_float(w[1])} * v1[2 * q];
+                        if (2 * q + 1 < OT)
+                            vall[2 * q + 1] = c2f{__uint_as_float(w[2]), __uint_as_float(w[3])} * v1[2 * q + 1];
+                    }
+                }
             } else if constexpr (CH == OT) {  // one load round: a thread's slot words and scaled z / phi, 16-byte loads
                 if (!C2_SKIP(32)) {
                     c2_ld_slots<OT>(rk, tl, kall);

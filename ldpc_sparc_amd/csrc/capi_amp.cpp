@@ -79,6 +79,7 @@ struct sg_amp_plan {
     uint32_t *c2_wab = nullptr, *c2_rab = nullptr;
     void *c2_cf = nullptr, *c2_gf = nullptr;
     float *c2_gm = nullptr;  // [OT][512][2] (|al|, |be|) of the polar row form (build_cw2)
+    float *c2_gmt = nullptr; // [512][OTP][2] the same, thread-major
     int c2_shoff = 0;        // log2(N / 2): unit of the slot's phase offset
     // its double-precision form (amp_cw2d.hip): coefficients, the slots' w_N2^a, the P-point twiddles
     double *c2d_cf = nullptr, *c2d_gf = nullptr, *c2d_sa = nullptr, *c2d_twp = nullptr;
@@ -788,6 +789,14 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
     p->c2_cf = dcf;
     p->c2_gf = dgf;
     SG_TRY(upload(p, &p->c2_gm, gm));
+    {  // thread-major copy of (|al|, |be|): thread tid's slots at [tid][OTP][2] (16-byte loads of two slots)
+        const int OTP = cw2_otp(OT);
+        std::vector<float> gmt((size_t)OTP * T * 2, 0.f);
+        for (int tid = 0; tid < T; ++tid)
+            for (int j = 0; j < OT; ++j)
+                for (int c = 0; c < 2; ++c) gmt[((size_t)tid * OTP + j) * 2 + c] = gm[((size_t)j * T + tid) * 2 + c];
+        SG_TRY(upload(p, &p->c2_gmt, gmt));
+    }
     p->c2_shoff = pow2 ? ilog2((int)(N / 2)) : 0;
     if (f64) {
         std::vector<double> twp((size_t)P * 2);
@@ -1100,6 +1109,7 @@ static Cw2Tables c2tables(const sg_amp_plan *p, int B) {
     tb.inv_n2 = 1.0f / (float)p->N2;
     tb.cmask = p->c2_cmask; tb.ka = p->c2_ka; tb.kat = p->c2_kat; tb.oi = p->c2_oi;
     tb.cf = (const float4 *)p->c2_cf; tb.gf = (const float4 *)p->c2_gf; tb.gm = (const float2 *)p->c2_gm;
+    tb.gmt = (const float4 *)p->c2_gmt;
     tb.sh_off = p->c2_shoff; tb.m4n = (uint32_t)(4 * p->w - 1); tb.inv_4n = (float)(1.0 / (4.0 * (double)p->w));
     tb.cls_ptr = p->r_cls_ptr; tb.cls_ls = p->r_cls_ls; tb.cls2 = p->c2_cls; tb.clsp = p->c2_clsp; tb.qpos = p->r_qpos; tb.seg = p->r_seg;
     tb.xr = (float *)p->ws_c2xp; tb.vz = (float *)p->ws_c2vz; tb.ys = (float *)p->ws_c2ys; tb.zs = (float *)p->ws_c2zs; tb.wab = (const uint2 *)p->c2_wab; tb.rab = (const uint2 *)p->c2_rab; tb.part = (float4 *)p->ws_c2part;
