@@ -791,10 +791,10 @@ def concat_bench(args, d):
             "roofline": {"bound": "mfma", "achieved": ach, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
                          "frac": ach / MFMA_F32_PEAK_TFS if ach else None,
                          "traffic": concat_traffic,
-                         "traffic_unit": "HBM bytes per gemm_f32_mfma launch (PMC FETCH_SIZE x2 + WRITE_SIZE, "
+                         "traffic_unit": "HBM bytes per GEMM launch (PMC FETCH_SIZE x2 + WRITE_SIZE, "
                                          f"profiles/{concat_tfile})" if concat_traffic else None,
                          "mfma_busy": concat_mfma,
-                         "kernel": "gemm_f32_mfma (A beta split-K NT + A^T z NN, v_mfma_f32_32x32x2_f32)",
+                         "kernel": "gemm_f32_glds (A beta split-K NT + A^T z NN, v_mfma_f32_32x32x2_f32, LDS-DMA staging)",
                          "algorithmic_flops_per_batch_iteration": 4.0 * n * L * M * B,
                          "kernel_ms": {k: round(v[0], 3) for k, v in ph.items()},
                          "launches": {k: v[1] for k, v in ph.items()}}}

@@ -1,4 +1,4 @@
-"""Summary of tools/pmc_concat.sh: per gemm_f32_mfma launch the HBM bytes
+"""Summary of tools/pmc_concat.sh: per GEMM launch (gemm_f32_glds / gemm_f32_mfma) the HBM bytes
 (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md gfx950 correction), the
 average duration from the kernel-trace stats, and the MFMA counters; merged as
 the "concat" section into the round's PMC traffic file (bench.py reads
@@ -29,7 +29,7 @@ def load(path):
     return agg, {k: len(v) for k, v in n.items()}
 
 
-gk = "gemm_f32_mfma"
+gk = "gemm_f32_"  # gemm_f32_glds (LDS-DMA staging, default) or gemm_f32_mfma
 f, nf = load(os.path.join(d, "f", "run_counter_collection.csv"))
 w, _ = load(os.path.join(d, "w", "run_counter_collection.csv"))
 fk = next(k for k in f if k.startswith(gk))
