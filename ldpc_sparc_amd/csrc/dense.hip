@@ -204,9 +204,19 @@ typedef __attribute__((address_space(3))) void lds_void;
 // one 16-byte-per-lane DMA global -> LDS (buffer_load_dwordx4 ... lds): lane i's 16 bytes land at lds + 16 i
 // (a non-template device function: the builtin inside the kernel template kept the host pass from emitting its
 // launch stubs)
+template <int AUX>
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, float *lds, int vo, int so) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void *)lds, 16, vo, so, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void *)lds, 16, vo, so, 0, AUX);
 }
+// the design matrix's DMAs non-temporal (aux 2: nt), as gemm_ld_y's loads, so the streamed A leaves the XCD's L2
+// before the batch operand every N tile re-reads (1), or default policy (0) (A/B).  Same box: default 0.873 / 0.872
+// of the f32 MFMA peak, nt 0.866 / 0.865 (the register-staged kernel 0.866 / 0.865); fabric bytes per NT launch
+// 37.5 GB (default) / 41.0 GB (nt): the batch operand is re-read past L2 either way, and the GEMM is MFMA-bound
+// (A once is 19.3 GB, 2.4 ms of an 18 ms launch at 8 TB/s) (profiles/r06_gemm_glds_ab.txt)
+#ifndef GEMM_GLDS_YNT
+#define GEMM_GLDS_YNT 0
+#endif
+constexpr int GLDS_YAUX = GEMM_GLDS_YNT ? 2 : 0;
 template <bool NT, int MT>
 __global__ __launch_bounds__(256, MT == 4 ? 2 : 1) void gemm_f32_glds(GemmF32 g) {
     constexpr int BM = gbm<MT>(), BUF = glds_buf_floats<MT>();
@@ -249,18 +259,18 @@ __global__ __launch_bounds__(256, MT == 4 ? 2 : 1) void gemm_f32_glds(GemmF32 g)
         // X: BM rows x 4 slots = BM / 16 wave-instructions of 16 rows
 #pragma unroll
         for (int i = 0; i < BM / 64; ++i)
-            dma16(rx, bx + 256 * (i * 4 + wid), ox[i], 4 * k0);
+            dma16<0>(rx, bx + 256 * (i * 4 + wid), ox[i], 4 * k0);
         if (NT) {  // 128 n-rows x 4 slots
 #pragma unroll
             for (int i = 0; i < 2; ++i)
-                dma16(ry, by + 256 * (i * 4 + wid), oy[i], 4 * k0);
+                dma16<GLDS_YAUX>(ry, by + 256 * (i * 4 + wid), oy[i], 4 * k0);
         } else {  // 16 k-rows x 128 n, two k-rows per wave-instruction (A is 19 GB at C5: a resource per tile)
             const int nrk = __builtin_amdgcn_readfirstlane(4 * ldy * max(0, min(GBK2, g.yrows - k0)));
             const __amdgpu_buffer_rsrc_t rk =
                 __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(g.Y + (long)k0 * ldy + n0), 0, nrk, 0x00020000);
 #pragma unroll
             for (int i = 0; i < 2; ++i)
-                dma16(rk, by + 256 * (i * 4 + wid), oy[i], 0);
+                dma16<GLDS_YAUX>(rk, by + 256 * (i * 4 + wid), oy[i], 0);
         }
     };
     f32x16 acc[MT][2];
