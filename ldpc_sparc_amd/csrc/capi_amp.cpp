@@ -501,6 +501,9 @@ static int build_cw(sg_amp_plan *p, const std::vector<int32_t> &row_k1, const st
 #ifndef CW2_BANKBAL
 #define CW2_BANKBAL 1
 #endif
+#ifndef CW2_BANKW
+#define CW2_BANKW 0
+#endif
 static void cw2_bank_balance(std::vector<std::vector<int>> &own, const std::vector<std::vector<int>> &pair_of,
                              int OT, int P) {
     const int T = CW2_THREADS;
@@ -516,7 +519,15 @@ static void cw2_bank_balance(std::vector<std::vector<int>> &own, const std::vect
             }
         }
     }
-    // the lanes of a group hold distinct pairs at a slot, so distinct rows; empty slots all read row 0
+    // the lanes of a group hold distinct pairs at a slot, so distinct rows; empty slots all read row 0.
+    // CW2_BANKW: cw2_az's row writes counted too -- ds_write_b64 serves 16-lane groups on 32 banks, so two
+    // lanes of one 16-lane half collide when their rows' slots agree mod 16 (padding slots write the
+    // thread's last pair again: C2_ROWS_ALWAYS)
+    auto last_row = [&](int t, int j) {
+        for (int q = j; q >= 0; --q)
+            if (at[(size_t)t * OT + q] >= 0) return at[(size_t)t * OT + q];
+        return 0;
+    };
     auto cell = [&](int g, int j) {
         int ca[32] = {0}, cb[32] = {0}, wa = 0, wb = 0;
         bool empty = false;
@@ -530,7 +541,19 @@ static void cw2_bank_balance(std::vector<std::vector<int>> &own, const std::vect
             wa = std::max(wa, ++ca[c2pos(ra) & 31]);
             if (rb != ra) wb = std::max(wb, ++cb[c2pos(rb) & 31]);
         }
-        return wa + wb;
+        int w = wa + wb;
+        if (CW2_BANKW) {
+            for (int hf = 0; hf < 2; ++hf) {
+                int sa[16] = {0}, sb[16] = {0}, xa = 0, xb = 0;
+                for (int l = 16 * hf; l < 16 * hf + 16; ++l) {
+                    const int ra = last_row(g * 32 + l, j), rb = (P - ra) % P;
+                    xa = std::max(xa, ++sa[c2pos(ra) & 15]);
+                    xb = std::max(xb, ++sb[c2pos(rb) & 15]);
+                }
+                w += xa + xb;
+            }
+        }
+        return w;
     };
     std::vector<std::vector<int>> by((size_t)OT * (OT + 1));
     for (int t = 0; t < T; ++t)

@@ -14,8 +14,8 @@ import json
 import os
 import sys
 
-LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ldpc_sparc_amd", "_lib",
-                   "libldpc_sparc_amd.so")
+LIB = os.environ.get("LDPC_SPARC_AMD_LIB") or os.path.join(  # the library the profiled run loaded
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ldpc_sparc_amd", "_lib", "libldpc_sparc_amd.so")
 
 
 def load(path, counter):

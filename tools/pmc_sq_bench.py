@@ -51,8 +51,8 @@ for k in sorted(a1):
               "lds_bank_conflict_frac": c.get("SQ_LDS_BANK_CONFLICT", 0) / lds,
               "lds_insts_per_wave": c.get("SQ_INSTS_LDS", 0) / max(c.get("SQ_WAVES", 1), 1),
               "valu_insts_per_wave": c.get("SQ_INSTS_VALU", 0) / max(c.get("SQ_WAVES", 1), 1)}
-LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ldpc_sparc_amd", "_lib",
-                   "libldpc_sparc_amd.so")
+LIB = os.environ.get("LDPC_SPARC_AMD_LIB") or os.path.join(  # the library the profiled run loaded
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ldpc_sparc_amd", "_lib", "libldpc_sparc_amd.so")
 res = {"kernels": out, "lib_sha256": hashlib.sha256(open(LIB, "rb").read()).hexdigest()[:16],
        "method": "rocprofv3 --pmc, two passes of 8 SQ counters over a short bench.py run (tools/pmc_sq_bench.sh: "
                  + os.environ.get("SQ_ARGS_USED", "") + "); fractions of SQ_WAVE_CYCLES (summed over waves)"}
