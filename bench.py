@@ -126,6 +126,9 @@ def parse():
     ap.add_argument("--concat-ebn0", type=float, default=5.5)
     ap.add_argument("--concat-n", type=int, default=9216,
                     help="C5 codeword length (9216: R_overall 0.58, decodable above ~5 dB Eb/N0)")
+    ap.add_argument("--timed-prof-level", type=int, default=2, choices=(0, 2),
+                    help="HIP-event scopes during the timed C2 steps: 2 (default) around every AMP iteration, "
+                         "0 none (A/B of the events' own cost; no roofline)")
     ap.add_argument("--cpu-seconds", type=float, default=60.0,
                     help="wall-time cap of the C2 CPU-baseline sample (the other legs scale from it; 0 disables)")
     ap.add_argument("--cpu-procs", type=int, default=0,
@@ -1047,7 +1050,7 @@ def main():
         if pf is not None:
             fine = pf.stop()
     _native.device_synchronize()
-    prof = _native.Profiler(level=2 if args.warmup > 0 else 1)
+    prof = _native.Profiler(level=2 if args.warmup > 0 else 1) if args.timed_prof_level else None
     d.barrier()
     _native.device_synchronize()
     t0 = time.perf_counter()
@@ -1055,7 +1058,7 @@ def main():
         amp_step(st, args, comm)
     _native.device_synchronize()
     el = time.perf_counter() - t0
-    phases = prof.stop()
+    phases = prof.stop() if prof is not None else {}
     el_max = d.max(el)
     cnt = st["d_cnt"].download(np.zeros(4, np.int64))  # last step, summed over ranks
     tf = st["d_tf"].download(np.zeros(st["B"], np.int32))
