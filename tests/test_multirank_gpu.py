@@ -37,6 +37,23 @@ def test_bench_two_ranks_rehearsal():
     assert full["amp"]["codeword_errors"] >= 0 and full["n_gpus"] == 2
 
 
+def test_bench_two_ranks_under_torchrun():
+    """The driver's launch form (python -m torch.distributed.run ... bench.py --gpus N): the ranks find rank 0's
+    host rendezvous through the run-keyed port file, not through the agent's MASTER_PORT store."""
+    env = {k: v for k, v in os.environ.items() if not k.startswith("SG_AMP_") and k != "SG_RDZV_PORT"}
+    env["BENCH_REHEARSAL"] = "1"
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                        os.path.join(REPO, "bench.py"), "--gpus", "2", "--no-bp", "--no-sc", "--no-sc-notebook",
+                        "--no-concat", "--no-r13", "--no-f64", "--cpu-seconds", "0", "--steps", "2", "--warmup", "1",
+                        "--batch", "64"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["counter_allreduce"].startswith("host") and out["value"] > 0
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
