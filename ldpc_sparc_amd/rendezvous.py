@@ -102,19 +102,26 @@ class HostGroup:
         try:
             while len(conns) < self.world:
                 c, _ = srv.accept()
-                c.settimeout(None)
+                c.settimeout(1.0)  # a peer that connects and never says hello must not stall the relay
                 try:
                     hello = json.loads(_recv(c))
-                except (ConnectionError, ValueError):
+                    ok = (isinstance(hello, dict) and hello.get("key") == self._key.decode()
+                          and isinstance(hello.get("rank"), int) and 0 <= hello["rank"] < self.world)
+                    _send(c, b"OK" if ok else b"NO")
+                except (OSError, ConnectionError, ValueError):
                     c.close()
                     continue
-                ok = hello.get("key") == self._key.decode() and 0 <= hello.get("rank", -1) < self.world
-                _send(c, b"OK" if ok else b"NO")
                 if ok:
+                    c.settimeout(None)
+                    old = conns.pop(int(hello["rank"]), None)  # a rank that retried: its newer connection
+                    if old is not None:
+                        old.close()
                     conns[int(hello["rank"])] = c
                 else:
                     c.close()
-        except OSError:
+        except OSError:  # the world never assembled: release the ranks that did connect
+            for c in conns.values():
+                c.close()
             return
         finally:
             srv.close()
@@ -143,10 +150,19 @@ class HostGroup:
                     p = None
             if p:
                 try:
+                    # (the handshake keeps a timeout: a stale port file may name a port that some other server
+                    # now holds, which would never answer; it is longer than the relay's 1 s per silent peer, so a
+                    # rank does not give up -- and leave a half-registered connection behind -- while the relay
+                    # is busy with another peer)
                     so = socket.create_connection((self.addr, p), timeout=5.0)
-                    so.settimeout(None)
-                    _send(so, json.dumps({"key": self._key.decode(), "rank": self.rank}).encode())
-                    if _recv(so) == b"OK":
+                    so.settimeout(15.0)
+                    try:
+                        _send(so, json.dumps({"key": self._key.decode(), "rank": self.rank}).encode())
+                        ok = _recv(so) == b"OK"
+                    except (OSError, ConnectionError):
+                        ok = False
+                    if ok:
+                        so.settimeout(None)
                         so.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
                         self._so = so
                         return

@@ -267,3 +267,41 @@ def test_compact_line_fits_the_driver(tmp_path):
     # the detail file holds the full record
     p = b.write_detail(out, str(tmp_path))
     assert json.load(open(os.path.join(REPO, p))) == out
+
+
+def test_rendezvous_survives_silent_and_foreign_peers():
+    """A peer that connects to the relay and never says hello, and one with the wrong key, are dropped; the
+    real ranks still meet (rendezvous.py handshake timeouts)."""
+    import socket as _so
+    import threading
+    from ldpc_sparc_amd.rendezvous import HostGroup, free_port
+    port = free_port()
+    out = {}
+
+    def rank(r):
+        g = HostGroup(r, 2, "127.0.0.1", port, timeout=60)
+        out[r] = g.allreduce_sum_i64([r + 1, 10 * r])
+        g.close()
+
+    t0 = threading.Thread(target=rank, args=(0,))
+    t0.start()
+    silent = None
+    for _ in range(200):  # the relay is up once rank 0 listens
+        try:
+            silent = _so.create_connection(("127.0.0.1", port), timeout=1.0)
+            break
+        except OSError:
+            import time
+            time.sleep(0.05)
+    assert silent is not None
+    foreign = _so.create_connection(("127.0.0.1", port), timeout=1.0)
+    body = b'{"key": "not-this-run", "rank": 1}'
+    foreign.sendall(len(body).to_bytes(8, "little") + body)
+    t1 = threading.Thread(target=rank, args=(1,))
+    t1.start()
+    t0.join(30)
+    t1.join(30)
+    silent.close()
+    foreign.close()
+    assert not t0.is_alive() and not t1.is_alive()
+    assert out[0].tolist() == [3, 10] and out[1].tolist() == [3, 10]
