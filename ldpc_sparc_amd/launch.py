@@ -20,6 +20,9 @@ import time
 from .rendezvous import free_port
 
 
+GRACE_S = 30.0
+
+
 def spawn(nproc, cmd, env=None, addr="127.0.0.1"):
     """Run cmd (an argv list) as nproc ranks; returns the job's exit code."""
     base = dict(os.environ if env is None else env)
@@ -30,6 +33,7 @@ def spawn(nproc, cmd, env=None, addr="127.0.0.1"):
                  MASTER_ADDR=addr, MASTER_PORT=str(port), SG_RDZV_PORT=str(port))
         procs.append(subprocess.Popen(cmd, env=e))
     code = 0
+    kill_at = None  # after a failure: SIGTERM to the others, SIGKILL to any still running GRACE_S later
     try:
         live = list(procs)
         while live:
@@ -39,9 +43,14 @@ def spawn(nproc, cmd, env=None, addr="127.0.0.1"):
                     continue
                 live.remove(p)
                 if rc != 0 and code == 0:
-                    code = rc
+                    code = rc if rc > 0 else 128 - rc  # killed by signal s: 128 + s, as a shell reports it
                     for q in live:  # a failed rank: the others would wait for it at the next rendezvous
                         q.send_signal(signal.SIGTERM)
+                    kill_at = time.monotonic() + GRACE_S
+            if kill_at is not None and time.monotonic() > kill_at:
+                for q in live:
+                    q.kill()
+                kill_at = None
             time.sleep(0.05)
     finally:
         for p in procs:

@@ -305,3 +305,20 @@ def test_rendezvous_survives_silent_and_foreign_peers():
     foreign.close()
     assert not t0.is_alive() and not t1.is_alive()
     assert out[0].tolist() == [3, 10] and out[1].tolist() == [3, 10]
+
+
+def test_launcher_stops_siblings_of_a_failed_rank(tmp_path, monkeypatch):
+    """Rank 1 exits 3; rank 0 ignores SIGTERM and would wait for it forever: the launcher returns 3 and
+    kills rank 0 after the grace period (ldpc_sparc_amd.launch.spawn)."""
+    import time
+    from ldpc_sparc_amd import launch
+    script = tmp_path / "rank.py"
+    script.write_text("import os, signal, sys, time\n"
+                      "if os.environ['RANK'] == '1':\n"
+                      "    time.sleep(0.5); sys.exit(3)\n"
+                      "signal.signal(signal.SIGTERM, signal.SIG_IGN)\n"
+                      "time.sleep(120)\n")
+    monkeypatch.setattr(launch, "GRACE_S", 1.0)
+    t0 = time.monotonic()
+    assert launch.spawn(2, [sys.executable, str(script)]) == 3
+    assert time.monotonic() - t0 < 30
