@@ -743,16 +743,6 @@ static int build_cw2(sg_amp_plan *p, const uint32_t *o0, double sc, const std::v
                 uint32_t &e = ka[(size_t)j * T + tid];
                 if (!(e & CW_VALID)) e = last_word[tid];
             }
-    // Padding slots (after a thread's pairs; zero coefficients, zero z/phi scale, not VALID) carry the word of
-    // the thread's last output without CW_NEWROW: the f32 rows (amp_cw2.hip, C2_ROWS_ALWAYS) write every
-    // slot's running sum at its pair's rows, so a padding slot adds 0 to the last pair's sums and writes them
-    // again -- never a row of another thread's pair
-    if (p->precision != SG_F64)
-        for (int tid = 0; tid < T; ++tid)
-            for (int j = 0; j < OT; ++j) {
-                uint32_t &e = ka[(size_t)j * T + tid];
-                if (!(e & CW_VALID)) e = last_word[tid];
-            }
     // Which image values the class scatter (Ab, class m2 < Q) and the row
     // writes (Az, entry Q) leave behind, as bits of the thread that reads
     // them in the first FFT stage (c2_stage0_r32: complex index m1 = j + 256 g

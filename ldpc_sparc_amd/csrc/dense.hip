@@ -377,8 +377,10 @@ __global__ __launch_bounds__(256, MT == 4 ? 2 : 1) void gemm_f32_glds(GemmF32 g)
 
 // the LDS-DMA kernel (1) or the register-staged one (0) (A/B); the DMA kernel only where its tiles are whole
 static bool glds_ok(const GemmF32 &g, bool nt) {
-    // whole K tiles, 16-byte aligned rows, whole NN column tiles, 32-bit per-block offsets
+    // whole K tiles, 16-byte aligned rows (aligned bases, row strides of 4 floats), whole NN column tiles,
+    // 32-bit per-block offsets
     return GEMM_GLDS && g.K % GBK2 == 0 && g.kchunk % GBK2 == 0 && g.ldx % 4 == 0 && g.ldy % 4 == 0 &&
+           ((uintptr_t)g.X % 16 == 0) && ((uintptr_t)g.Y % 16 == 0) &&
            (nt || g.N % GBN == 0) && g.M > 0 && g.yrows > 0 && 4.0 * g.ldx * gbm<4>() < 2147483647.0 &&
            4.0 * g.ldy * GBN < 2147483647.0;
 }
