@@ -3,8 +3,8 @@
 // xGMI.  The reference has no multi-process path (independent processes per
 // sim_id, ldpc_jossy/py/ldpc_awgn.py:125-131); this is the single collective
 // the decoding engine needs.  The unique id is produced by
-// rank 0 and handed to the other ranks by the host launcher (bench.py uses the
-// torch.distributed gloo store, CPU only).
+// rank 0 and handed to the other ranks over the host rendezvous
+// (ldpc_sparc_amd/rendezvous.py: standard-library TCP, no PyTorch).
 #include <rccl/rccl.h>
 
 #include <cstring>

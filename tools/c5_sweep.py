@@ -70,7 +70,7 @@ def main():
     ap.add_argument("--L-unprotected", type=int, default=160)
     ap.add_argument("--mults", type=int, default=4)
     ap.add_argument("--rehearsal", action="store_true",
-                    help="CPU only: gloo counters and a synthetic trial instead of RCCL and the GPU pipeline")
+                    help="CPU only: host-rendezvous counters and a synthetic trial instead of RCCL and the GPU pipeline")
     ap.add_argument("--max-rounds", type=int, default=None, help="interrupt every point after this many rounds")
     args = ap.parse_args()
     world, rank = int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))
