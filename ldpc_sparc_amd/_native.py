@@ -214,11 +214,14 @@ class DeviceBuffer:
 
     def upload(self, arr, stream=None):
         arr = np.ascontiguousarray(arr)
-        assert arr.nbytes <= self.nbytes
+        if arr.nbytes > self.nbytes:  # (a real check, not an assert: python -O must not drop it)
+            raise ValueError(f"upload of {arr.nbytes} bytes into a {self.nbytes}-byte device buffer")
         check(lib().sg_memcpy_h2d(self.ptr, ptr(arr), arr.nbytes, stream))
 
     def download(self, out, stream=None):
-        assert out.flags.c_contiguous and out.nbytes <= self.nbytes
+        if not out.flags.c_contiguous or out.nbytes > self.nbytes:
+            raise ValueError(f"download into a {'non-contiguous ' if not out.flags.c_contiguous else ''}"
+                             f"{out.nbytes}-byte array from a {self.nbytes}-byte device buffer")
         check(lib().sg_memcpy_d2h(ptr(out), self.ptr, out.nbytes, stream))
         return out
 
@@ -305,7 +308,8 @@ class Comm:
         return bytes(buf)
 
     def __init__(self, nranks, rank, uid):
-        assert len(uid) == Comm.ID_BYTES
+        if len(uid) != Comm.ID_BYTES:
+            raise ValueError(f"RCCL unique id of {len(uid)} bytes, expected {Comm.ID_BYTES}")
         self._id = (ct.c_char * Comm.ID_BYTES).from_buffer_copy(uid)
         h = ct.c_void_p()
         check(lib().sg_comm_init(int(nranks), int(rank), ct.cast(self._id, ct.c_void_p), ct.byref(h)))

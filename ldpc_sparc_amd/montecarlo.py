@@ -39,8 +39,12 @@ class Aggregator:
     rehearsals (`group`, a `rendezvous.HostGroup`)."""
 
     def __init__(self, backend="none", comm=None, group=None):
-        assert backend in ("none", "host", "rccl")
-        assert backend != "host" or group is not None, "the host backend needs a rendezvous group"
+        if backend not in ("none", "host", "rccl"):
+            raise ValueError(f"Aggregator backend {backend!r}: one of none, host, rccl")
+        if backend == "host" and group is None:
+            raise ValueError("the host backend needs a rendezvous group")
+        if backend == "rccl" and comm is None:
+            raise ValueError("the rccl backend needs a communicator (_native.Comm)")
         self.backend = backend
         self.comm = comm
         self.group = group
