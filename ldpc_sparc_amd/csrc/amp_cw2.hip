@@ -118,6 +118,14 @@ static_assert(C2_EPT == 16, "the transform is written for 16 values per thread")
 #ifndef C2_ST_BITS
 #define C2_ST_BITS 1
 #endif
+// Az statistics: segment entries read per lane in the first round, the rest in rounds of as many until the
+// wavefront's longest segment is done (segments average LM / (Q L) = 8 entries).  The entries are summed in
+// segment order whatever the round size, so every choice gives bit-identical statistics.  Three calls of three
+// interleaved rounds (profiles/r06_c2_stats_rounds_ab.txt): 12 is 2 % slower than 16 (the round-5 form, one
+// round covering nearly every segment), 2 to 8 are faster; 4: 0.840 -> 0.830 ms per iteration, C2 +1.2 % (default)
+#ifndef C2_RC
+#define C2_RC 4
+#endif
 // Az rows' per-codeword class-invariant input (a thread's scaled z / phi, 24 VGPRs at 12 slots) loaded once per
 // launch and held in registers across the class loop (1; with the statistics launch cw2_az has the registers),
 // or re-read from L2 / MALL every class (0) (A/B); the slot words are the plan's, shared by every codeword
@@ -1073,9 +1081,9 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
             // partial of the section over its segment: the maximum, then the
             // sums of e and e^2 over every entry but one maximum
             // (e = exp((x - max) / tau)); two passes instead of the online
-            // rescaling (fewer vector instructions).  The first 16 entries are
+            // rescaling (fewer vector instructions).  The first C2_RC entries are
             // read once for both passes (segments average LM / (Q L) = 8
-            // entries; longer ones take the loops below), the reads are
+            // entries; the rest take the loops below), the reads are
             // unskewed (every read a base plus a constant; the segment starts
             // are irregular either way) and entries past the segment are -inf
             // (exp -> 0).  Same box, every codeword active (tools/c2_ablate.py,
@@ -1083,7 +1091,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
             // cw2_az; unconditional reads, the fract form below and the rows'
             // derived addresses took cw2_az 0.588 -> 0.570 ms per launch.
             const int a = sa[k], n = sb[k] - sa[k];
-            constexpr int RC = 16;
+            constexpr int RC = C2_RC;
             const float *sgp = dr + a;  // inside the LDS image past the segment's end too
             float x[RC];
             // every read unconditional, the entries past the segment masked afterwards: written as

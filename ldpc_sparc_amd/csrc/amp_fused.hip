@@ -24,6 +24,12 @@
 // beta itself never reaches HBM: it is recomputed from s where needed.
 #include "amp.hpp"
 
+// reg_az_stage2 statistics: segment entries per round of LDS reads (entries summed in segment order for any
+// round size: bit-identical results) (A/B)
+#ifndef FUSED_RC
+#define FUSED_RC 16
+#endif
+
 namespace sg {
 
 template <typename T>
@@ -471,7 +477,7 @@ __global__ __launch_bounds__(reg_s1_threads(EPT, LOG2P)) void reg_az_stage2(RegT
     T *pm = bf.part + (((size_t)cw * tb.nT + t) * tb.Q + m2) * 3 * (size_t)tb.Lblk;
     // one thread per section over its contiguous segment (segments average
     // ~16 entries: the fpad skew spreads the threads over the LDS banks)
-    constexpr int RC = 16;  // LDS reads in flight per thread
+    constexpr int RC = FUSED_RC;  // LDS reads in flight per thread
     for (int l = tid; l < ((tb.skip & 8) ? 0 : tb.Lblk); l += nthr) {
         const int a = sg[l], b = sg[l + 1];
         if constexpr (kRestSums<T>) {
