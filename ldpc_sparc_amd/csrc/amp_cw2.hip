@@ -126,6 +126,13 @@ static_assert(C2_EPT == 16, "the transform is written for 16 values per thread")
 #ifndef C2_RC
 #define C2_RC 4
 #endif
+// Az statistics: every round of reads in the two loops, none held in registers across the maximum (1), or a
+// first round read once for both passes (0) (A/B; bit-identical).  Two same-box calls of three rounds: +0.4 %,
+// +0.2 % (profiles/r06_c2_stats_rounds_ab.txt); the two sections' rounds interleaved in one pair of loops
+// measured 2 % slower
+#ifndef C2_NOFIRST
+#define C2_NOFIRST 1
+#endif
 // Az rows' per-codeword class-invariant input (a thread's scaled z / phi, 24 VGPRs at 12 slots) loaded once per
 // launch and held in registers across the class loop (1; with the statistics launch cw2_az has the registers),
 // or re-read from L2 / MALL every class (0) (A/B); the slot words are the plan's, shared by every codeword
@@ -1092,6 +1099,31 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
             // derived addresses took cw2_az 0.588 -> 0.570 ms per launch.
             const int a = sa[k], n = sb[k] - sa[k];
             constexpr int RC = C2_RC;
+#if C2_NOFIRST
+            // every round in the loops (no first round held in registers across the maximum)
+            float m = -INFINITY;
+            for (int c = 0; c < n; c += RC) {
+                float y[RC];
+#pragma unroll
+                for (int i = 0; i < RC; ++i) y[i] = dr[a + c + i];
+#pragma unroll
+                for (int i = 0; i < RC; ++i) m = fmaxf(m, c + i < n ? y[i] : -INFINITY);
+            }
+            float S1 = 0.f, S2 = 0.f, Se = 0.f;
+            for (int c = 0; c < n; c += RC) {
+                float y[RC];
+#pragma unroll
+                for (int i = 0; i < RC; ++i) y[i] = dr[a + c + i];
+#pragma unroll
+                for (int i = 0; i < RC; ++i) {
+                    const float ex = c2_exp2(((c + i < n ? y[i] : -INFINITY) - m) * inv_tau);
+                    const float f = __builtin_amdgcn_fractf(ex);
+                    S1 += f;
+                    S2 += f * f;
+                    Se += ex;
+                }
+            }
+#else
             const float *sgp = dr + a;  // inside the LDS image past the segment's end too
             float x[RC];
             // every read unconditional, the entries past the segment masked afterwards: written as
@@ -1157,6 +1189,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
                     Se += ex;
                 }
             }
+#endif
             {
                 const float ties = rintf(Se - S1) - 1.f;  // entries equal to the maximum, but one (NaN: empty)
                 if (ties > 0.f) {
