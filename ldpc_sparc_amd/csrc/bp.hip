@@ -6,8 +6,9 @@
 // per 1944-bit block.
 //
 // Design (DESIGN.md "BP kernel"):
-//   * one 256-thread workgroup decodes one codeword at a time, persistent over
-//     the batch (grid = occupancy x CUs, codewords pulled by blockIdx stride);
+//   * one workgroup decodes one codeword at a time: one workgroup per codeword
+//     for single-precision min-sum, persistent over the batch otherwise
+//     (grid = occupancy x CUs, codewords pulled by blockIdx stride; BPF_GRID_B);
 //   * the whole message state of the codeword lives in LDS for all
 //     iterations: HBM sees only the channel LLRs (read once per iteration
 //     through L2) and the final a-posteriori LLRs;
@@ -27,6 +28,15 @@
 #include <algorithm>
 
 #include "bp.hpp"
+
+// table kernels, single-precision min-sum: one workgroup per codeword (1), or a persistent grid of (workgroups
+// per CU) x CUs looping over the batch with the graph tables staged once per workgroup (0) (A/B).  Same box
+// (profiles/r06_bp_grid_ab.txt): 802.11n r5/6 z = 81 (the lean kernel) 6.54 M -> 7.07 M codewords/s; the
+// double-precision sum-product kernels lose 6 % with it (their table staging per codeword), so they stay
+// persistent
+#ifndef BPF_GRID_B
+#define BPF_GRID_B 1
+#endif
 
 namespace sg {
 
@@ -377,7 +387,7 @@ static int launch_one(const BpArgs<T> &a, size_t lds, hipStream_t s) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BP_THREADS, lds) != hipSuccess || per_cu < 1)
         per_cu = 1;
     int grid = per_cu * device_cu_count();
-    if (grid > a.B) grid = a.B;
+    if ((BPF_GRID_B && sizeof(T) == 4 && KIND == SG_MINSUM) || grid > a.B) grid = a.B;
     if (lds > 64 * 1024)
         SG_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     ProfScope ps(SG_PH_BP, s);

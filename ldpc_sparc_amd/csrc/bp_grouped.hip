@@ -32,6 +32,15 @@
 // kernel (capi_ldpc.cpp), the device entry point documents it.
 #include "bp.hpp"
 
+// one workgroup per codeword (1: the hardware dispatcher hands each finished workgroup's CU slot to the next
+// codeword; a workgroup's LDS image starts uninitialised, which the first iteration's read-free variable pass
+// and the per-iteration flag words allow), or a persistent grid of (workgroups per CU) x CUs looping over the
+// batch (0) (A/B).  Same box, two calls (profiles/r06_bp_grid_ab.txt): C3 5.91 M -> 6.24 M and 5.94 M -> 6.34 M
+// codewords/s, 0.62-0.63 -> 0.66-0.67 of the LDS bound, bit-identical
+#ifndef BPG_GRID_B
+#define BPG_GRID_B 1
+#endif
+
 namespace sg {
 
 // Channel LLRs are saturated at this magnitude on load (far beyond any LLR a
@@ -419,7 +428,7 @@ static int grouped_one(const BpGrpArgs &a, hipStream_t s) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BP_THREADS, lds) != hipSuccess || per_cu < 1)
         per_cu = 1;
     int grid = per_cu * device_cu_count();
-    if (grid > a.B) grid = a.B;
+    if (BPG_GRID_B || grid > a.B) grid = a.B;
     if (lds > 64 * 1024)
         SG_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     ProfScope ps(SG_PH_BP, s);

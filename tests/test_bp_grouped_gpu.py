@@ -180,11 +180,11 @@ def test_overflowing_channel_input_stays_finite(monkeypatch):
 
 
 @pytest.mark.parametrize("ebn0", [1.0, 2.0])
-def test_c3_batch_every_workgroup_decodes_several_codewords(monkeypatch, ebn0):
-    """C3 at its bench size (B = 4096, BASELINE.json configs[2]): the grouped
-    kernel's grid is 4 workgroups per CU (bp_grouped.hip:228), so each
-    workgroup decodes B / grid codewords in turn, reusing its LDS image and its
-    parity-buffered stop flags.  Bit for bit against the float32 restatement of
+def test_c3_batch_at_bench_size(monkeypatch, ebn0):
+    """C3 at its bench size (B = 4096, BASELINE.json configs[2]): one workgroup
+    per codeword (bp_grouped.hip BPG_GRID_B), 4096 workgroups through 4 slots
+    per CU, so later workgroups start on LDS images and stop-flag words that
+    earlier ones left behind.  Bit for bit against the float32 restatement of
     the corrected min-sum (c_ldpc.c:339-381) at iteration caps 1 and 50."""
     c = code("802.11n", "1/2", 81)
     B = 4096
