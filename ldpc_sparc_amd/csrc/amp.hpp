@@ -201,6 +201,11 @@ size_t cw_lds_bytes(int img, int nslots);
 // j < OT, grouped by conjugate row pair {r, P - r} of the P-point stage (host
 // build_cw2).  See DESIGN.md "Split per-codeword engine".
 constexpr int CW2_THREADS = 512;
+// f32 split engine: workgroups per codeword at most (Cw2Tables.np: 2, or 4 once codewords have stopped), each
+// taking Q / np of the classes; the partial buffers are sized for CW2_NP
+#ifndef CW2_NP
+#define CW2_NP 4
+#endif
 constexpr int CW2_SLICE = 9216;     // class entries per workgroup pass (18 per thread)
 // P-point image layout of the split engine: complex element i at c2pos(i) =
 // i + i / 32 (one pad value per 32), so every LDS access of the transform's
@@ -219,6 +224,7 @@ __host__ __device__ constexpr int cw2_otp(int ot) { return (ot + 3) & ~3; }
 __host__ __device__ constexpr bool cw2_vz_tm(int ot) { return ot <= 12; }
 struct Cw2Tables {
     int L, M, LM, n, N2, Q, Lblk, OT, maxcls;
+    int np;                   // workgroups per codeword (f32 split engine): 2, or 4 once codewords have stopped
     float inv_n2;             // 1 / N2
     const uint32_t *cmask;    // [Q + 1][512] image values each thread's first FFT stage reads (class m2; rows: Q)
     const uint32_t *ka;       // [OT][512] a | CW_VALID | CW_NEWROW (first of its pair) | CW_ENDROW | CW_SELF

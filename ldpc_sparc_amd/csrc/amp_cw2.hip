@@ -133,6 +133,7 @@ static_assert(C2_EPT == 16, "the transform is written for 16 values per thread")
 #ifndef C2_NOFIRST
 #define C2_NOFIRST 1
 #endif
+// workgroups per codeword: tb.np (amp.hpp CW2_NP: at most 8, the largest of 8, 4, 2 dividing Q)
 // Az rows' per-codeword class-invariant input (a thread's scaled z / phi, 24 VGPRs at 12 slots) loaded once per
 // launch and held in registers across the class loop (1; with the statistics launch cw2_az has the registers),
 // or re-read from L2 / MALL every class (0) (A/B); the slot words are the plan's, shared by every codeword
@@ -451,7 +452,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float *dr = reinterpret_cast<float *>(smem);
     c2f *sMI = reinterpret_cast<c2f *>(smem + C2_IMG_BYTES);  // previous beta's (section max, 1 / sum)
-    const int h = blockIdx.x & 1, cw = blockIdx.x >> 1, tid = threadIdx.x;
+    const int h = blockIdx.x % tb.np, cw = blockIdx.x / tb.np, tid = threadIdx.x;
     if (!bf.active[cw]) return;
     C2_SETPRIO(C2_PRIO_REST);
     const size_t lb = (size_t)cw * tb.L;
@@ -463,7 +464,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
     cx<float> Ha[OT], Hb[OT];  // H[a], conj H[b] of the thread's outputs over this half's classes
 #pragma unroll
     for (int j = 0; j < OT; ++j) Ha[j] = Hb[j] = {0.f, 0.f};
-    const int Qh = tb.Q >> 1;
+    const int Qh = tb.Q / tb.np;
     c2_tw1_init<false>(tid);
     const int *cpl = c2_stage_cp(smem, tb, tid);
     __syncthreads();  // the staged statistics
@@ -571,7 +572,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_ab(Cw2Tables tb, RegBufs<float> b
     C2_TP(11);
     // this half's part of the forward output Re(c1 H[a] + c2 conj H[b]) (linear in H: cw2_ctrl adds the
     // two halves' parts; a quarter of the bytes of the partial H pair)
-    float *xr = tb.xr + ((size_t)cw * 2 + h) * OT * C2_T;
+    float *xr = tb.xr + ((size_t)cw * tb.np + h) * OT * C2_T;
 #pragma unroll
     for (int j = 0; j < OT; ++j) {
         const float4 c = tb.cf[j * C2_T + tid];
@@ -640,7 +641,7 @@ __global__ __launch_bounds__(C2_T) void cw2_ctrl(Cw2Tables tb, RegBufs<float> bf
         g = pr.W[0];
         if (tid == 0) sc.gamma[cw] = g;
     }
-    const float *xr0 = tb.xr + (size_t)cw * 2 * OT * C2_T, *xr1 = xr0 + (size_t)OT * C2_T;
+    const float *xr0 = tb.xr + (size_t)cw * tb.np * OT * C2_T, *xr1 = xr0 + (size_t)OT * C2_T;
     float zr[OT];
     float2 gmv[C2_POLAR ? OT : 1];
     double acc = 0.0;
@@ -660,6 +661,7 @@ __global__ __launch_bounds__(C2_T) void cw2_ctrl(Cw2Tables tb, RegBufs<float> bf
                 zv[j] = zs[j * C2_T + tid];
                 r0[j] = xr0[j * C2_T + tid];
                 r1[j] = xr1[j * C2_T + tid];
+                for (int pp = 2; pp < tb.np; ++pp) r1[j] += xr0[(size_t)pp * OT * C2_T + j * C2_T + tid];
             }
 #pragma unroll
             for (int j = 0; j < OT; ++j)  // Onsager residual, sparc.py:943-946; r = Re(c1 H[a] + c2 conj H[b])
@@ -755,7 +757,7 @@ template <int OT>
 __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> bf, int t) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float *dr = reinterpret_cast<float *>(smem);
-    const int h = blockIdx.x & 1, cw = blockIdx.x >> 1, tid = threadIdx.x;
+    const int h = blockIdx.x % tb.np, cw = blockIdx.x / tb.np, tid = threadIdx.x;
     if (!bf.active[cw]) return;
     C2_SETPRIO(C2_PRIO_REST);
     const size_t lb = (size_t)cw * tb.L;
@@ -782,7 +784,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
     (void)Lb;
     (void)inv_tau;
 #endif
-    const int Qh = tb.Q >> 1;
+    const int Qh = tb.Q / tb.np;
     c2_tw1_init<true>(tid);
     const int *cpl = c2_stage_cp(smem, tb, tid);
     constexpr bool HOLD = C2_AZ_HOLD && C2_POLAR && OT <= 12;
@@ -1219,7 +1221,7 @@ __global__ __launch_bounds__(C2_T, 4) void cw2_az(Cw2Tables tb, RegBufs<float> b
     }
     C2_TP(43);
 #if !C2_STATS_LAUNCH
-    float4 *part = tb.part + ((size_t)cw * 2 + h) * Lb;
+    float4 *part = tb.part + ((size_t)cw * tb.np + h) * Lb;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         const int sec = tid + k * C2_T;
@@ -1360,11 +1362,14 @@ __global__ __launch_bounds__(1024) void cw2_merge(Cw2Tables tb, RegBufs<float> b
     const float inv_tau = (float)(C2_LOG2E / bf.tau[cw]);  // log2 e / tau (c2_exp2)
     double a = 0.0, er = 0.0;
     if (tid < Lb) {
-        const float4 *part = tb.part + (size_t)cw * 2 * Lb;
+        const float4 *part = tb.part + (size_t)cw * tb.np * Lb;
         float Mr = -INFINITY, R1 = 0.f, R2 = 0.f, s_true = NAN;
-        const float4 ph[2] = {part[tid], part[Lb + tid]};  // (both requested together)
+        float4 ph[CW2_NP];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {  // the halves in order: same merge as the class merge of cw2_az
+        for (int h = 0; h < CW2_NP; ++h)  // (all requested together)
+            ph[h] = h < tb.np ? part[h * Lb + tid] : make_float4(-INFINITY, 0.f, 0.f, NAN);
+#pragma unroll
+        for (int h = 0; h < CW2_NP; ++h) {  // the parts in order: same merge as the class merge of cw2_az
             const float4 p = ph[h];
             const float m = p.x;
             if (!(p.w != p.w)) s_true = p.w;
@@ -1450,7 +1455,7 @@ static int cw2_launch(const Cw2Tables &tb, const RegBufs<float> &bf, const AmpSc
                                    (int)C2_LDS_BYTES) == hipSuccess;
     }();
     if (!ready) return fail(SG_ERR_HIP, "split per-codeword engine: kernel attributes (static LDS / LDS size)");
-    const dim3 g2(2 * bf.B), gB(bf.B);
+    const dim3 g2(tb.np * bf.B), gB(bf.B);
     if (t > 0) {
         ProfScope ps(SG_PH_CW2_AB, s);
         hipLaunchKernelGGL((cw2_ab<OT>), g2, dim3(C2_T), lds, s, tb, bf);

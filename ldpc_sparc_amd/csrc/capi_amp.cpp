@@ -74,6 +74,7 @@ struct sg_amp_plan {
     uint32_t *c_kt = nullptr;
     // split per-codeword engine (amp_cw2.hip): outputs per thread (0 = not built) and its tables
     int cw2OT = 0;
+    int c2_np = 2;                // f32 split engine: workgroups per codeword for the next launches (decode_regular)
     uint32_t *c2_ka = nullptr, *c2_kat = nullptr, *c2_cmask = nullptr, *c2_cls = nullptr, *c2_clsp = nullptr;
     int32_t *c2_oi = nullptr;
     uint32_t *c2_wab = nullptr, *c2_rab = nullptr;
@@ -225,11 +226,11 @@ static int ensure_ws(sg_amp_plan *p, int B, int t_max) {
             SG_HIP(hipMemset(p->tprof, 0, p->tprof_items * 20 * sizeof(uint64_t)));
         }
         if (p->cw2OT) {  // (reals of the plan's precision; partial statistics: four per section)
-            SG_ALLOC(p->ws_c2xp, Bz * 2 * p->cw2OT * CW2_THREADS * rs);
+            SG_ALLOC(p->ws_c2xp, Bz * std::max(CW2_NP, 2) * p->cw2OT * CW2_THREADS * rs);
             SG_ALLOC(p->ws_c2vz, Bz * cw2_otp(p->cw2OT) * CW2_THREADS * 8);  // (f32: two reals per slot)
             SG_ALLOC(p->ws_c2ys, Bz * p->cw2OT * CW2_THREADS * rs);
             SG_ALLOC(p->ws_c2zs, Bz * p->cw2OT * CW2_THREADS * rs);
-            SG_ALLOC(p->ws_c2part, Bz * 2 * p->Lblk * 4 * rs);
+            SG_ALLOC(p->ws_c2part, Bz * std::max(CW2_NP, 2) * p->Lblk * 4 * rs);
             if (p->precision == SG_F64) {
                 SG_ALLOC(p->ws_c2beta, Bz * p->LM * rs);
                 SG_ALLOC(p->ws_c2sec, Bz * p->L * 2 * rs);
@@ -498,6 +499,10 @@ static int build_cw(sg_amp_plan *p, const std::vector<int32_t> &row_k1, const st
 // of the cells they touch does not grow.  Every output keeps its arithmetic (same slot structure per
 // thread, same class order); only the order of cw2_ctrl's sum of z^2 (phi) follows the placement.
 // Deterministic (fixed seed).
+// f32 split engine: four workgroups per codeword once codewords have stopped (1), always two (0) (A/B)
+#ifndef C2_PARTS_ADAPT
+#define C2_PARTS_ADAPT 1
+#endif
 #ifndef CW2_BANKBAL
 #define CW2_BANKBAL 1
 #endif
@@ -1111,7 +1116,7 @@ static CwTables ctables(const sg_amp_plan *p, int B) {
     tb.stw = (const cx<float> *)p->c_stw;
     tb.inv_n2 = 1.0f / (float)p->N2;
     // [B][32] stamps, only when the diagnostics buffer holds them
-    tb.tprof = (p->tprof && p->tprof_items * 20 >= (size_t)32 * B) ? p->tprof : nullptr;
+    tb.tprof = (p->tprof && p->tprof_items * 20 >= (size_t)64 * CW2_NP * B) ? p->tprof : nullptr;  // (64 per workgroup)
     return tb;
 }
 
@@ -1119,6 +1124,8 @@ static Cw2Tables c2tables(const sg_amp_plan *p, int B) {
     Cw2Tables tb;
     tb.L = p->L; tb.M = p->M; tb.LM = p->LM; tb.n = p->n; tb.N2 = p->N2; tb.Q = p->rQ; tb.Lblk = p->Lblk;
     tb.OT = p->cw2OT; tb.maxcls = p->rmaxcls;
+    // (build_cw2: Q even; the decode loop asks for more than two once codewords have stopped)
+    tb.np = p->c2_np >= 4 && CW2_NP >= 4 && p->rQ % 4 == 0 ? 4 : 2;
     tb.inv_n2 = 1.0f / (float)p->N2;
     tb.cmask = p->c2_cmask; tb.ka = p->c2_ka; tb.kat = p->c2_kat; tb.oi = p->c2_oi;
     tb.cf = (const float4 *)p->c2_cf; tb.gf = (const float4 *)p->c2_gf; tb.gm = (const float2 *)p->c2_gm;
@@ -1622,6 +1629,11 @@ static int decode_regular(sg_amp_plan *p, const void *d_y, int B, const int32_t 
     pr.phi_method = phi_method; pr.t_max = t_max;
     SG_TRY(reg_launch_init(B, p->Lc, t_max, p->ws_nmse, p->ws_active, p->ws_tfinal, s));
     ActivePoll poll{p, B, s};
+    // f32 split engine: two workgroups per codeword (each half of the classes) while every codeword is active;
+    // once the active-flag poll shows stopped codewords, four, so the dispatcher refills the CU slots of the
+    // stopped ones (same box: R = 1.3 +4 %, profiles/r06_c2_parts_ab.txt; four from the start cost the
+    // all-active R = 1.5 line 0.2-0.8 %: the control kernel sums twice the parts)
+    p->c2_np = 2;
     // (double precision has the split engine only: SG_AMP_CW2=0 leaves it the staged engine)
     bool cw = use_cw(p, B) && (std::is_same<T, float>::value || use_cw2(p));
     p->last_engine = cw ? 2 : 1;
@@ -1657,6 +1669,7 @@ static int decode_regular(sg_amp_plan *p, const void *d_y, int B, const int32_t 
         int na = -1;
         SG_TRY(poll.collect(&na));  // the flags after iteration t - 1
         if (na == 0) break;
+        if (na > 0 && na < B && C2_PARTS_ADAPT) p->c2_np = 4;
         if (na > 0 && cw && !cw_forced && na < handover * B) {
             cw = false;
             p->last_handover = t + 1;  // first iteration on the staged engine
